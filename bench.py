@@ -1,0 +1,183 @@
+#!/usr/bin/env python
+"""Headline benchmark: audio-seconds/sec of whisper-large-v3 greedy generate, 30 s clips, batch 32/GPU.
+
+One step = one batch of 32 synthetic 30 s clips resident in HBM -> log-mel (HIP) -> encoder ->
+cross-K/V -> greedy decode (4-token prompt, max_length 128 -> 128 new tokens, hipGraph step) on the
+MI355X engine (bf16).  Weights are random-init of the large-v3 architecture (no checkpoints offline).
+N > 1: one process per GPU (torchrun), each rank decodes its own batches (data parallel, weak
+scaling), token ids are all-gathered over RCCL at the end (run_pseudo_labelling.py:339-341), and the
+time is the max over ranks.
+
+Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` of the dominant kernel (cross-attention
+K/V streaming, HBM-bound), ``encoder_mfma`` (encoder MFMA fraction), ``cpu_baseline`` (reference
+transformers path on the host cores, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "kotoba-whisper_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA spec
+ENC_FLOP_PER_CLIP = 2.2738e12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--max-length", type=int, default=128)
+    ap.add_argument("--model", default="large-v3")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--kernel-iters", type=int, default=20)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from kwhisper.config import PRESETS
+    from kwhisper.feature_extraction import WhisperFeatureExtractor
+    from kwhisper.generation import KWhisperForConditionalGeneration
+    from kwhisper.synthetic import dummy_audio, synthetic_state_dict_torch
+    from kwhisper import ops
+
+    shape = PRESETS[a.model]
+    sd = synthetic_state_dict_torch(shape, seed=0, device=dev)
+    model = KWhisperForConditionalGeneration.from_state_dict(shape, sd, dtype=torch.bfloat16, device=dev)
+    del sd
+    torch.cuda.empty_cache()
+    fe = WhisperFeatureExtractor(feature_size=shape.num_mel_bins, device=dev)
+    B = a.batch
+    audio = torch.from_numpy(np.stack([dummy_audio(rank * 100003 + i) for i in range(B)])).to(dev)
+
+    gen_kw = dict(language="ja", task="transcribe", max_length=a.max_length, return_timestamps=False)
+    out_ids = []
+
+    def step():
+        feats = fe.extract(audio)
+        ids = model.generate(feats, **gen_kw)
+        out_ids.append(ids)
+        return ids
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    new_tokens = int(out_ids[-1].shape[1])
+
+    # DP gather of the token matrices (the reference's pad_across_processes + gather_for_metrics, C4/C5)
+    ids = torch.stack(out_ids[-a.steps:]).to(torch.int32)
+    if world > 1:
+        L = torch.tensor([ids.shape[-1]], device=dev)
+        dist.all_reduce(L, op=dist.ReduceOp.MAX)
+        pad = torch.full((*ids.shape[:-1], int(L.item())), 50256, dtype=torch.int32, device=dev)
+        pad[..., : ids.shape[-1]] = ids
+        gathered = [torch.empty_like(pad) for _ in range(world)]
+        dist.all_gather(gathered, pad)
+
+    # ---- per-kernel measurements (HIP events on the launching stream, after the timed region) ----
+    eng = model.engine
+    sess = model._sessions[B]
+    stream = torch.cuda.current_stream(dev)
+    iters = a.kernel_iters
+
+    def time_fn(fn, n):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        fn()
+        e0.record(stream)
+        for _ in range(n):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1) / n * 1e-3
+
+    H, S, hd = eng.H, shape.max_source_positions, 64
+    qx = sess._buffers(1)["qx"]
+    attn_out = sess._buffers(1)["attn"]
+    ws = sess._buffers(1)["ws"]
+    cross_t = time_fn(lambda: ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[0], sess.cross[1], S, attn_out, ws), iters)
+    cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
+    feats = fe.extract(audio)
+    enc_t = time_fn(lambda: eng.encode(feats), 3)
+    step_graph = sess._graph
+    step_t = time_fn(lambda: step_graph.replay(), iters) if step_graph is not None else None
+    ms_per_step = dt / a.steps * 1e3
+
+    result = {
+        "metric": "audio-seconds/sec (RTF) whisper-large-v3 30s@bs32",
+        "value": world * B * 30.0 * a.steps / dt,
+        "unit": "audio-s/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (run_speed_eval.py noise audio, random-init large-v3 weights)",
+        "config": {"workload": "config 3: whisper-large-v3 greedy generate, 30 s clips, log-mel on GPU",
+                   "model": shape.name, "global_batch": B * world, "per_gpu_batch": B,
+                   "max_length": a.max_length, "new_tokens": new_tokens, "seq_len": 1500,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"kernel": "cross_attn_partial (decoder cross-attention K/V stream, per layer)",
+                     "bound": "hbm", "achieved": cross_bytes / cross_t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": cross_bytes / cross_t / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "bytes_per_launch": cross_bytes, "avg_launch_us": cross_t * 1e6},
+        "encoder_mfma": {"ms": enc_t * 1e3, "tflops": ENC_FLOP_PER_CLIP * B / enc_t / 1e12,
+                         "frac": ENC_FLOP_PER_CLIP * B / enc_t / 1e12 / BF16_PEAK_TFLOPS},
+        "decode_step_ms": step_t * 1e3 if step_t else None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle.cpu_baseline import hf_cpu_generate_rate
+
+        cb = hf_cpu_generate_rate(shape, a.cpu_batch, a.max_length)
+        result["cpu_baseline"] = {
+            "value": cb["audio_seconds_per_second"], "unit": "audio-s/s", "cores": cb["threads"], "kind": "reference",
+            "sample": f"transformers 5.15.0 WhisperForConditionalGeneration.generate fp32 on CPU, {a.cpu_batch} "
+                      f"clips x 30 s, greedy, {cb['new_tokens']} new tokens, {cb['seconds']:.1f} s"}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

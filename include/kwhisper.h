@@ -1,0 +1,147 @@
+/*
+ * kwhisper -- C ABI of the MI355X (gfx950) Whisper teacher hot path.
+ *
+ * Drop-in boundary: the Python host (kotoba-whisper_amd/kwhisper) binds these entry points with
+ * ctypes and exposes HF's WhisperForConditionalGeneration.generate() / WhisperFeatureExtractor API
+ * (SURVEY.md §8b).  Every pointer below is a DEVICE pointer unless stated; the caller owns all
+ * memory (kernels never allocate); every call is asynchronous on `stream` (a hipStream_t, 0 =
+ * null stream) and is safe to capture in a hipGraph.  Return value: KW_OK or a KW_E* code;
+ * kw_last_error() gives the message.  Nothing throws across the ABI.
+ *
+ * Element types: KW_DT_F32 = float32, KW_DT_BF16 = bfloat16 (raw uint16 storage).
+ * Reference interfaces each entry point replaces are cited as TF/<file>:<line>, where
+ * TF = transformers 5.15.0 (the arithmetic of kotoba-whisper's hot path, run_pseudo_labelling.py:338).
+ */
+#ifndef KWHISPER_H
+#define KWHISPER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* kw_stream_t;
+
+enum { KW_OK = 0, KW_EINVAL = 1, KW_EHIP = 2, KW_EUNSUPPORTED = 3 };
+enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
+enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
+
+/* ABI version (major*100 + minor) and the last error message of this thread. */
+int kw_version(void);
+const char* kw_last_error(void);
+
+/* a1 -- log-mel spectrogram.
+ * Replaces WhisperFeatureExtractor._torch_extract_fbank_features (TF/models/whisper/
+ * feature_extraction_whisper.py:135-168): stft(n_fft 400, hop 160, periodic hann, center, reflect)
+ * -> |X|^2 -> drop last frame -> mel_filters.T @ P -> log10(clamp 1e-10) -> per-clip max(x, max-8)
+ * -> (x+4)/4.   audio: [batch][audio_stride] f32 (first n_samples used, n_samples % 160 == 0,
+ * already padded/truncated as in __call__ :300-307); mel_filters: [201][n_mels] f32;
+ * out: [batch][n_mels][n_samples/160] f32; workspace: >= 4*batch bytes. */
+int kw_log_mel(const float* audio, int64_t batch, int64_t n_samples, int64_t audio_stride,
+               const float* mel_filters, int n_mels, float* out, void* workspace, kw_stream_t stream);
+
+/* Conv stem input re-layout: mel [B][C][T] f32 -> time-major, zero-padded [B][T+2][c_pad] (dtype),
+ * so that Conv1d(k=3, p=1) is a GEMM whose im2col row t is the contiguous 3*c_pad slice at row t
+ * (TF/models/whisper/modeling_whisper.py:566-567,618-619). */
+int kw_mel_to_time_major(const float* mel, int64_t B, int64_t C, int64_t T, int64_t c_pad,
+                         void* out, int out_dtype, kw_stream_t stream);
+
+/* Linear / conv-as-GEMM:  C = epilogue(A . W^T + bias)  (nn.Linear, TF modeling_whisper.py:279-282,
+ * 375-376, 444-445, 499-503, 566-567, 1080).
+ * Row maps: logical row r of A lives at A + (r / a_rows_per_batch)*a_batch_stride
+ * + (r % a_rows_per_batch)*lda (elements); the same for C.  W: [N][K] (or packed, kw_gemv).
+ * Epilogues: STORE  C = act(acc + bias) * (col < scale_cols ? scale : 1) (+ row_add[r % period][col])
+ *            RESID  C(f32) += acc + bias           (residual add, TF modeling_whisper.py:398,407)
+ *            HEADSPLIT  as STORE, written to C[part][b][h][t][d] with part = col / (heads*head_dim),
+ *                       b = r / hs_seq, t = r % hs_seq  (q/k/v and cross-K/V cache layout). */
+typedef struct {
+  int dtype;                 /* A and W element type */
+  int c_dtype;               /* C element type (RESID: must be KW_DT_F32) */
+  const void* A;
+  int64_t lda, a_rows_per_batch, a_batch_stride;
+  const void* W;
+  const float* bias;         /* [N] or NULL */
+  void* C;
+  int64_t ldc, c_rows_per_batch, c_batch_stride;
+  int64_t M, N, K;
+  int epilogue;              /* KW_EPI_* */
+  int gelu;                  /* exact-erf GELU after bias */
+  float scale;               /* applied to columns [0, scale_cols) after bias/GELU */
+  int64_t scale_cols;
+  const float* row_add;      /* [period][N] f32 added after the activation, or NULL */
+  int64_t row_add_period;
+  int64_t hs_seq, hs_heads, hs_head_dim;
+} kw_gemm_args;
+
+int kw_gemm(const kw_gemm_args* args, kw_stream_t stream);
+
+/* Skinny GEMM for decode steps (M <= 128): same contract as kw_gemm (STORE / RESID epilogues,
+ * no row maps), W pre-packed by kw_pack_weight (bf16 only). */
+int kw_gemv(const kw_gemm_args* args, kw_stream_t stream);
+/* W [N][K] bf16 -> packed [ceil(N/16)][K/32][64 lanes][8] bf16 (rows >= N zero); K % 32 == 0. */
+int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed, kw_stream_t stream);
+size_t kw_packed_weight_bytes(int64_t N, int64_t K);
+
+/* LayerNorm (eps) over the last dim of x [rows][dim] f32 -> y [rows][dim] (y_dtype);
+ * TF modeling_whisper.py:371,377,434,443,446,642,790. dim % 4 == 0, dim <= 2048. */
+int kw_layernorm(const float* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
+                 float eps, void* y, int y_dtype, kw_stream_t stream);
+
+/* Encoder self-attention softmax(Q K^T) V (q pre-scaled; TF sdpa_attention.py:79-166, non-causal).
+ * qkv: [3][B][H][T][hd] (dtype), out: [B][T][H*hd] (dtype). hd == 64. */
+int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, int64_t T, int64_t hd, void* out,
+                 kw_stream_t stream);
+
+/* Decoder input embedding: h[b*q_len+i] = tok_emb[ids[b][L-q_len+i]] + pos_emb[L-q_len+i]
+ * with L = *cur_len read on device (TF modeling_whisper.py:737-762; no embed scale). */
+int kw_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
+             const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
+             kw_stream_t stream);
+
+/* Decoder self-attention over a static cache (TF modeling_whisper.py:469-480, cache_utils.py:127-145):
+ * appends k/v of the q_len newest positions [L-q_len, L) to k_cache/v_cache [B][H][t_max][hd],
+ * then causal attention for those positions. qkv: [B*q_len][3*H*hd]; out [B*q_len][H*hd]. */
+int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t q_len, int64_t H, int64_t hd,
+                      void* k_cache, void* v_cache, int64_t t_max, const int32_t* cur_len, void* out,
+                      kw_stream_t stream);
+
+/* Decoder cross-attention against cached encoder K/V [B][H][S][hd] (TF modeling_whisper.py:323-326).
+ * q: [B*q_len][H*hd]; out: [B*q_len][H*hd]; workspace >= kw_cross_attn_workspace(...) bytes. */
+int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64_t H, int64_t hd,
+                       const void* k, const void* v, int64_t S, void* out, void* workspace,
+                       size_t ws_bytes, kw_stream_t stream);
+size_t kw_cross_attn_workspace(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S);
+
+/* One greedy decoding step on f32 logits [B][V] (TF generation/utils.py:2894-2937):
+ * SuppressTokens -> SuppressTokensAtBegin (when L == begin_index) -> WhisperTimeStamp (if
+ * return_timestamps; TF generation/logits_process.py:1816-2047) -> argmax (first max) ->
+ * finished rows emit pad -> ids[b][L] = token; unfinished[b] updated (EOS / L+1 >= max_length);
+ * the last workgroup advances *cur_len and writes *n_unfinished.  suppress_mask: [V] uint8 (1 = suppressed).
+ * scores_out: optional [B][V] f32 copy of the processed scores (NULL to skip). */
+typedef struct {
+  float* logits;
+  int64_t B, V;
+  const uint8_t* suppress_mask;
+  const int32_t* begin_suppress;
+  int32_t n_begin_suppress;
+  int32_t return_timestamps;
+  int32_t ts_begin, no_ts_id, eos_id, pad_id;
+  int32_t max_initial_ts;     /* -1 = None */
+  int64_t* ids;               /* [B][ids_stride] */
+  int64_t ids_stride;
+  int32_t* cur_len;
+  int32_t max_length, begin_index;
+  int32_t* unfinished;        /* [B] */
+  int32_t* counter;           /* [1] scratch, zero before first use */
+  int32_t* n_unfinished;      /* [1] rows still unfinished after this step (written by the last workgroup) */
+  float* scores_out;
+} kw_sampler_args;
+
+int kw_greedy_step(const kw_sampler_args* args, kw_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KWHISPER_H */

@@ -1,0 +1,510 @@
+// Attention kernels for the Whisper hot path on gfx950.
+//
+// Encoder (K6): flash-style bf16 attention, non-causal, T = 1500, head_dim 64
+// (TF/models/whisper/modeling_whisper.py:284-356 + TF/integrations/sdpa_attention.py:79-166;
+// q arrives pre-scaled by head_dim^-0.5 from the QKV epilogue, modeling_whisper.py:309).
+//   Per workgroup: one (batch, head, 128-query tile); 4 waves x 32 queries.  Scores are computed
+//   TRANSPOSED, S^T = K Q^T (v_mfma_f32_32x32x16_bf16), so each lane owns one query's scores and the
+//   row softmax needs only in-lane math plus one lane^32 exchange.  O^T = V^T P^T takes P^T straight
+//   from the S^T accumulators (no LDS round trip) and V^T from a row-major V tile through
+//   ds_read_b64_tr_b16.  K/V tiles (64 keys) are staged global->LDS by global_load_lds_dwordx4 into a
+//   2-deep ring with XOR-swizzled images (K: chunk ^ ((row>>1)&7) for ds_read_b128; V: chunk ^
+//   (((row>>1)&1)<<2) for the transposed reads) -- both conflict-free.  O is normalised and staged
+//   through LDS for 16-B coalesced stores.
+// Encoder f32 path: exact-fp32 reference-order kernel for the parity mode.
+// Decoder self-attention (K10): static KV cache append + causal attention (q_len >= 1).
+// Decoder cross-attention (K11): split-S partial softmax over cached encoder K/V, 8 lanes per key row
+//   so every K and V load is a coalesced 1-KB wave access; partials combined in a second kernel.
+#include <math.h>
+
+#include "kw_common.h"
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+
+namespace {
+
+constexpr float LOG2E = 1.4426950408889634f;
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
+
+// ------------------------------------------------------------------------------------------------
+// encoder flash attention, bf16
+// ------------------------------------------------------------------------------------------------
+constexpr int AQ = 128;        // queries per workgroup
+constexpr int AK = 64;         // keys per tile
+constexpr int HD = 64;
+constexpr int TILE_BYTES = AK * HD * 2;  // 8 KB
+constexpr int ATT_LDS = 2 * 2 * TILE_BYTES;  // K,V x 2 stages = 32 KB (O staging reuses it)
+
+__global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict__ qkv, int B, int H, int T,
+                                                       bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char smem[ATT_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_qt = (T + AQ - 1) / AQ;
+  const int bh = blockIdx.x / n_qt;
+  const int qt = blockIdx.x - bh * n_qt;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const int64_t head_elems = (int64_t)T * HD;
+  const bf16_t* Q = qkv + ((int64_t)(0 * B + b) * H + h) * head_elems;
+  const bf16_t* K = qkv + ((int64_t)(1 * B + b) * H + h) * head_elems;
+  const bf16_t* V = qkv + ((int64_t)(2 * B + b) * H + h) * head_elems;
+
+  const int q_lane = qt * AQ + wave * 32 + (lane & 31);
+  const int hh = lane >> 5;
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[q][16s + 8h .. +7]
+  bf16x8 qf[4];
+  {
+    const int qr = min(q_lane, T - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)qr * HD + 16 * s + 8 * hh);
+  }
+
+  // staging: each tile (64 rows x 128 B) = 8 glds instructions; wave w issues rows [16w, 16w+16)
+  const int n_kt = (T + AK - 1) / AK;
+  auto stage = [&](int s, int kt) {
+    char* kb = smem + s * 2 * TILE_BYTES;
+    char* vb = kb + TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int g = wave * 2 + i;  // 8-row group
+      const int row = 8 * g + (lane >> 3);
+      const int key = min(kt * AK + row, T - 1);
+      const int slot = lane & 7;
+      const int ck = slot ^ ((row >> 1) & 7);
+      const int cv = slot ^ (((row >> 1) & 1) << 2);
+      glds16(K + (int64_t)key * HD + ck * 8, kb + g * 1024);
+      glds16(V + (int64_t)key * HD + cv * 8, vb + g * 1024);
+    }
+  };
+
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = -INFINITY, l_run = 0.f;
+
+  stage(0, 0);
+  for (int kt = 0; kt < n_kt; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < n_kt) stage((kt + 1) & 1, kt + 1);
+    const char* kb = smem + (kt & 1) * 2 * TILE_BYTES;
+    const char* vb = kb + TILE_BYTES;
+
+    // S^T for 2 key blocks of 32
+    f32x16 st[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) st[i][r] = 0.f;
+      const int row = i * 32 + (lane & 31);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int c = 2 * s + hh;
+        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+        st[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[i], 0, 0, 0);
+      }
+    }
+    // mask keys >= T (last tile only), row max
+    const int key0 = kt * AK;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int key = key0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        if (key >= T) st[i][r] = -INFINITY;
+        mx = fmaxf(mx, st[i][r]);
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = exp2f((m_run - m_new) * LOG2E);
+    const float mneg = -m_new * LOG2E;
+    float rs = 0.f;
+    bf16x8 pf[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float p = exp2f(fmaf(st[i][8 * s + e], LOG2E, mneg));
+          rs += p;
+          pf[i][s][e] = (__bf16)p;
+        }
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+
+    // O^T += V^T P^T ; A operand via ds_read_b64_tr_b16 from the row-major V tile
+    const int li = lane & 15, qq = li >> 2, pp = li & 3, grp = (lane >> 4) & 1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)        // key block
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {    // 16-key step
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {  // hd block
+          bf16x8 vf;
+#pragma unroll
+          for (int half = 0; half < 2; ++half) {
+            const int row = i * 32 + 16 * s + 8 * half + 4 * hh + qq;
+            const int chunk = db * 4 + 2 * grp + (pp >> 1);
+            const int off = row * 128 + ((chunk ^ (((row >> 1) & 1) << 2)) << 4) + (pp & 1) * 8;
+            const s16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+                (__attribute__((address_space(3))) s16x4*)(vb + off));
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              short sv = t[e];
+              vf[4 * half + e] = *reinterpret_cast<__bf16*>(&sv);
+            }
+          }
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[i][s], o[db], 0, 0, 0);
+        }
+      }
+  }
+
+  // normalise and stage O (q rows x 64 hd, bf16) through LDS for coalesced stores
+  __syncthreads();
+  bf16_t* os = reinterpret_cast<bf16_t*>(smem) + wave * 32 * HD;  // 4 KB per wave
+  const float inv_l = 1.0f / l_run;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = db * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      os[(lane & 31) * HD + d] = f2bf(o[db][r] * inv_l);
+    }
+  __syncthreads();
+  // each wave writes its 32 rows x 128 B: 256 16-B chunks, 4 per lane
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int chunk = i * 64 + lane;
+    const int qr = chunk >> 3, cc = chunk & 7;
+    const int q = qt * AQ + wave * 32 + qr;
+    if (q < T) {
+      const uint4 v = *reinterpret_cast<const uint4*>(os + qr * HD + cc * 8);
+      *reinterpret_cast<uint4*>(out + ((int64_t)b * T + q) * (H * HD) + h * HD + cc * 8) = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// encoder attention, f32 (parity mode): 4 waves = 4 queries share K/V tiles in LDS
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_fwd_f32(const float* __restrict__ qkv, int B, int H, int T,
+                                                   float* __restrict__ out) {
+  __shared__ float ks[64][HD + 1];
+  __shared__ float vs[64][HD + 1];
+  __shared__ float qs[4][HD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n_qb = (T + 3) / 4;
+  const int bh = blockIdx.x / n_qb, qb = blockIdx.x - bh * n_qb;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const int64_t head_elems = (int64_t)T * HD;
+  const float* Q = qkv + ((int64_t)(0 * B + b) * H + h) * head_elems;
+  const float* K = qkv + ((int64_t)(1 * B + b) * H + h) * head_elems;
+  const float* V = qkv + ((int64_t)(2 * B + b) * H + h) * head_elems;
+  const int q = qb * 4 + wave;
+  qs[wave][lane] = Q[(int64_t)min(q, T - 1) * HD + lane];
+  float m = -INFINITY, l = 0.f, acc = 0.f;
+  for (int k0 = 0; k0 < T; k0 += 64) {
+    __syncthreads();
+    for (int i = tid; i < 64 * HD; i += 256) {
+      const int r = i >> 6, c = i & 63;
+      const int key = min(k0 + r, T - 1);
+      ks[r][c] = K[(int64_t)key * HD + c];
+      vs[r][c] = V[(int64_t)key * HD + c];
+    }
+    __syncthreads();
+    float s = 0.f;
+#pragma unroll 16
+    for (int c = 0; c < HD; ++c) s = fmaf(qs[wave][c], ks[lane][c], s);
+    if (k0 + lane >= T) s = -INFINITY;
+    const float mt = wave_max(s);
+    const float mn = fmaxf(m, mt);
+    const float alpha = expf(m - mn);
+    const float p = expf(s - mn);
+    l = l * alpha + wave_sum(p);
+    acc *= alpha;
+    for (int j = 0; j < 64; ++j) acc = fmaf(__shfl(p, j, 64), vs[j][lane], acc);
+    m = mn;
+  }
+  if (q < T) out[((int64_t)b * T + q) * (H * HD) + h * HD + lane] = acc / l;
+}
+
+// ------------------------------------------------------------------------------------------------
+// decoder self-attention: append to static cache, then causal attention (q_len >= 1)
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) void self_attn_step(const T* __restrict__ qkv, int q_len, int H, int hd,
+                                                      T* __restrict__ kc, T* __restrict__ vc, int t_max,
+                                                      const int32_t* __restrict__ cur_len, T* __restrict__ out) {
+  __shared__ float sc[512];
+  __shared__ float qv[64];
+  __shared__ float red[4][64];
+  __shared__ float stat[2];
+  const int bh = blockIdx.x;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const int tid = threadIdx.x;
+  const int L = *cur_len;
+  const int d = H * hd;
+  const int64_t cbase = ((int64_t)b * H + h) * t_max * hd;
+  // append k, v of the q_len newest positions
+  for (int i = tid; i < q_len * hd; i += 256) {
+    const int qi = i / hd, c = i - (i / hd) * hd;
+    const int p = L - q_len + qi;
+    const T* row = qkv + ((int64_t)b * q_len + qi) * 3 * d;
+    kc[cbase + (int64_t)p * hd + c] = row[d + h * hd + c];
+    vc[cbase + (int64_t)p * hd + c] = row[2 * d + h * hd + c];
+  }
+  __syncthreads();
+  for (int qi = 0; qi < q_len; ++qi) {
+    const int p = L - q_len + qi;  // attends keys [0, p]
+    const int nk = p + 1;
+    const T* qrow = qkv + ((int64_t)b * q_len + qi) * 3 * d + h * hd;
+    if (tid < hd) qv[tid] = TypeIO<T>::ld(qrow + tid);
+    __syncthreads();
+    float mx = -INFINITY;
+    for (int k = tid; k < nk; k += 256) {
+      const T* kr = kc + cbase + (int64_t)k * hd;
+      float s = 0.f;
+      for (int c = 0; c < hd; ++c) s = fmaf(qv[c], TypeIO<T>::ld(kr + c), s);
+      sc[k] = s;
+      mx = fmaxf(mx, s);
+    }
+    mx = wave_max(mx);
+    if ((tid & 63) == 0) red[tid >> 6][0] = mx;
+    __syncthreads();
+    if (tid == 0) stat[0] = fmaxf(fmaxf(red[0][0], red[1][0]), fmaxf(red[2][0], red[3][0]));
+    __syncthreads();
+    const float m = stat[0];
+    float sum = 0.f;
+    for (int k = tid; k < nk; k += 256) {
+      const float e = expf(sc[k] - m);
+      sc[k] = e;
+      sum += e;
+    }
+    sum = wave_sum(sum);
+    __syncthreads();
+    if ((tid & 63) == 0) red[tid >> 6][0] = sum;
+    __syncthreads();
+    if (tid == 0) stat[1] = (red[0][0] + red[1][0]) + (red[2][0] + red[3][0]);
+    __syncthreads();
+    const float inv = 1.0f / stat[1];
+    // O[c] = sum_k p_k V[k][c]; thread -> (c = tid & 63, key group tid >> 6)
+    const int c = tid & 63, g = tid >> 6;
+    float acc = 0.f;
+    if (c < hd)
+      for (int k = g; k < nk; k += 4) acc = fmaf(sc[k], TypeIO<T>::ld(vc + cbase + (int64_t)k * hd + c), acc);
+    red[g][c] = acc;
+    __syncthreads();
+    if (tid < hd) {
+      const float v = ((red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid])) * inv;
+      TypeIO<T>::st(out + ((int64_t)b * q_len + qi) * d + h * hd + tid, v);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// decoder cross-attention: split-S partials + combine
+// ------------------------------------------------------------------------------------------------
+constexpr int XS_MAX_CHUNK = 512;
+
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float v[8]);
+template <>
+__device__ __forceinline__ void load8<bf16_t>(const bf16_t* p, float v[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+template <>
+__device__ __forceinline__ void load8<float>(const float* p, float v[8]) {
+  const float4 a = reinterpret_cast<const float4*>(p)[0], b = reinterpret_cast<const float4*>(p)[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void cross_attn_partial(const T* __restrict__ q, int q_len, int H,
+                                                          const T* __restrict__ kc, const T* __restrict__ vc, int S,
+                                                          int chunk, float* __restrict__ ws) {
+  __shared__ float sc[XS_MAX_CHUNK];
+  __shared__ float red[32][64 + 1];
+  __shared__ float stat[8];
+  const int row = blockIdx.x;  // (b*q_len + qi)*H + h
+  const int split = blockIdx.y;
+  const int h = row % H;
+  const int bq = row / H;
+  const int b = bq / q_len;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = lane & 7, g = lane >> 3;
+  const int kslot = wave * 8 + g;  // 0..31
+  const int k0 = split * chunk;
+  const int k1 = min(S, k0 + chunk);
+  const int64_t base = ((int64_t)b * H + h) * S * HD;
+  float qv[8];
+  {
+    const T* qr = q + (int64_t)bq * H * HD + h * HD + sub * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) qv[i] = TypeIO<T>::ld(qr + i);
+  }
+  // scores
+  float mx = -INFINITY;
+  for (int k = k0 + kslot; k < k1; k += 32) {
+    float kv[8];
+    load8<T>(kc + base + (int64_t)k * HD + sub * 8, kv);
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s = fmaf(qv[i], kv[i], s);
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    s += __shfl_xor(s, 4, 64);
+    if (sub == 0) sc[k - k0] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) stat[wave] = mx;
+  __syncthreads();
+  const float m = fmaxf(fmaxf(stat[0], stat[1]), fmaxf(stat[2], stat[3]));
+  float sum = 0.f;
+  for (int k = tid; k < k1 - k0; k += 256) {
+    const float e = expf(sc[k] - m);
+    sc[k] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  if (lane == 0) stat[4 + wave] = sum;
+  __syncthreads();
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int k = k0 + kslot; k < k1; k += 32) {
+    float vv[8];
+    load8<T>(vc + base + (int64_t)k * HD + sub * 8, vv);
+    const float p = sc[k - k0];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = fmaf(p, vv[i], acc[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[kslot][sub * 8 + i] = acc[i];
+  __syncthreads();
+  float* w = ws + ((int64_t)row * gridDim.y + split) * (HD + 2);
+  if (tid < HD) {
+    float o = 0.f;
+    for (int s = 0; s < 32; ++s) o += red[s][tid];
+    w[2 + tid] = o;
+  }
+  if (tid == 0) {
+    w[0] = m;
+    w[1] = (stat[4] + stat[5]) + (stat[6] + stat[7]);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void cross_attn_combine(const float* __restrict__ ws, int nsplit, int H,
+                                                        T* __restrict__ out) {
+  const int row = blockIdx.x;  // (bq)*H + h
+  const int h = row % H, bq = row / H;
+  const int d = threadIdx.x;
+  const float* w = ws + (int64_t)row * nsplit * (HD + 2);
+  float M = -INFINITY;
+  for (int s = 0; s < nsplit; ++s) M = fmaxf(M, w[s * (HD + 2)]);
+  float l = 0.f, o = 0.f;
+  for (int s = 0; s < nsplit; ++s) {
+    const float f = expf(w[s * (HD + 2)] - M);
+    l = fmaf(w[s * (HD + 2) + 1], f, l);
+    o = fmaf(w[s * (HD + 2) + 2 + d], f, o);
+  }
+  TypeIO<T>::st(out + (int64_t)bq * H * HD + h * HD + d, o / l);
+}
+
+int cross_splits(int64_t S) {
+  int ns = (int)((S + 255) / 256);
+  if (ns < 1) ns = 1;
+  return ns;
+}
+
+}  // namespace
+
+extern "C" int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, int64_t T, int64_t hd, void* out,
+                            kw_stream_t stream) {
+  if (!qkv || !out || B <= 0 || H <= 0 || T <= 0) return kw_set_error_msg(KW_EINVAL, "kw_attention: invalid arguments");
+  if (hd != HD) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_attention: head_dim must be 64");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == KW_DT_BF16) {
+    const int64_t grid = B * H * ((T + AQ - 1) / AQ);
+    hipLaunchKernelGGL(attn_fwd_bf16, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)qkv, (int)B, (int)H, (int)T,
+                       (bf16_t*)out);
+  } else if (dtype == KW_DT_F32) {
+    const int64_t grid = B * H * ((T + 3) / 4);
+    hipLaunchKernelGGL(attn_fwd_f32, dim3((unsigned)grid), dim3(256), 0, s, (const float*)qkv, (int)B, (int)H, (int)T,
+                       (float*)out);
+  } else {
+    return kw_set_error_msg(KW_EUNSUPPORTED, "kw_attention: dtype");
+  }
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}
+
+extern "C" int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t q_len, int64_t H, int64_t hd,
+                                 void* k_cache, void* v_cache, int64_t t_max, const int32_t* cur_len, void* out,
+                                 kw_stream_t stream) {
+  if (!qkv || !k_cache || !v_cache || !cur_len || !out || B <= 0 || q_len <= 0 || H <= 0 || hd <= 0 || hd > 64 ||
+      t_max <= 0 || t_max > 512)
+    return kw_set_error_msg(KW_EINVAL, "kw_self_attn_step: invalid arguments (hd <= 64, t_max <= 512)");
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == KW_DT_BF16)
+    hipLaunchKernelGGL(self_attn_step<bf16_t>, dim3((unsigned)(B * H)), dim3(256), 0, s, (const bf16_t*)qkv, (int)q_len,
+                       (int)H, (int)hd, (bf16_t*)k_cache, (bf16_t*)v_cache, (int)t_max, cur_len, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(self_attn_step<float>, dim3((unsigned)(B * H)), dim3(256), 0, s, (const float*)qkv, (int)q_len,
+                       (int)H, (int)hd, (float*)k_cache, (float*)v_cache, (int)t_max, cur_len, (float*)out);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}
+
+extern "C" size_t kw_cross_attn_workspace(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S) {
+  (void)hd;
+  return (size_t)(B * q_len * H) * cross_splits(S) * (HD + 2) * sizeof(float);
+}
+
+extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64_t H, int64_t hd,
+                                  const void* k, const void* v, int64_t S, void* out, void* workspace, size_t ws_bytes,
+                                  kw_stream_t stream) {
+  if (!q || !k || !v || !out || !workspace || B <= 0 || q_len <= 0 || H <= 0 || S <= 0)
+    return kw_set_error_msg(KW_EINVAL, "kw_cross_attn_step: invalid arguments");
+  if (hd != HD) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_cross_attn_step: head_dim must be 64");
+  if (ws_bytes < kw_cross_attn_workspace(B, q_len, H, hd, S))
+    return kw_set_error_msg(KW_EINVAL, "kw_cross_attn_step: workspace too small");
+  const int ns = cross_splits(S);
+  const int chunk = (int)((S + ns - 1) / ns);
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)(B * q_len * H), (unsigned)ns);
+  if (dtype == KW_DT_BF16) {
+    hipLaunchKernelGGL(cross_attn_partial<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
+                       (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, (float*)workspace);
+    KW_CHECK_LAUNCH();
+    hipLaunchKernelGGL(cross_attn_combine<bf16_t>, dim3((unsigned)(B * q_len * H)), dim3(64), 0, s,
+                       (const float*)workspace, ns, (int)H, (bf16_t*)out);
+  } else {
+    hipLaunchKernelGGL(cross_attn_partial<float>, grid, dim3(256), 0, s, (const float*)q, (int)q_len, (int)H,
+                       (const float*)k, (const float*)v, (int)S, chunk, (float*)workspace);
+    KW_CHECK_LAUNCH();
+    hipLaunchKernelGGL(cross_attn_combine<float>, dim3((unsigned)(B * q_len * H)), dim3(64), 0, s,
+                       (const float*)workspace, ns, (int)H, (float*)out);
+  }
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}

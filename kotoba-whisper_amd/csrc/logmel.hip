@@ -1,0 +1,144 @@
+// a1 -- Whisper log-mel spectrogram on gfx950.
+//
+// Replaces WhisperFeatureExtractor._torch_extract_fbank_features
+// (TF/models/whisper/feature_extraction_whisper.py:135-168).  Per workgroup: FT consecutive STFT
+// frames of one clip.  The reflect-padded audio span of those frames is staged once in LDS
+// (coalesced 16-B loads), the windowed 400-point DFT is evaluated against an LDS twiddle table,
+// |X|^2 stays in LDS, the slaney mel projection reads the (L2-resident) filter bank, and log10 is
+// written time-contiguous.  The per-clip maximum is an order-preserving integer atomicMax; a second
+// light pass applies max(x, max-8) and (x+4)/4.
+//
+// Roofline: 1.12 GFLOP and 1.92 MB in / 1.54 MB out per clip -> compute-light; the
+// DFT runs on the VALU with f64 accumulation.
+#include <math.h>
+
+#include "kw_common.h"
+
+namespace {
+
+constexpr int N_FFT = 400;
+constexpr int HOP = 160;
+constexpr int N_BINS = N_FFT / 2 + 1;  // 201
+constexpr int FT = 32;                 // frames per workgroup
+constexpr int SPAN = (FT - 1) * HOP + N_FFT;  // 5360 samples
+constexpr int THREADS = 256;
+
+__device__ __forceinline__ uint32_t f2key(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+  uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+  return __uint_as_float(u);
+}
+
+__global__ __launch_bounds__(THREADS) void logmel_kernel(const float* __restrict__ audio, int64_t n_samples,
+                                                         int64_t audio_stride, const float* __restrict__ fb,
+                                                         int n_mels, float* __restrict__ out, int n_out,
+                                                         uint32_t* __restrict__ clip_max) {
+  __shared__ float xs[SPAN];
+  __shared__ double cosw[N_FFT];
+  __shared__ double sinw[N_FFT];
+  __shared__ double win[N_FFT];
+  __shared__ float pw[FT][N_BINS + 3];
+  __shared__ uint32_t red[THREADS / 64];
+
+  const int b = blockIdx.y;
+  const int f0 = blockIdx.x * FT;
+  const float* x = audio + (int64_t)b * audio_stride;
+  const int tid = threadIdx.x;
+  const float two_pi_n = 6.283185307179586476925 / N_FFT;
+
+  for (int i = tid; i < N_FFT; i += THREADS) {
+    double a = 6.283185307179586476925 * (double)i / N_FFT;
+    cosw[i] = cos(a);
+    sinw[i] = sin(a);
+    win[i] = (double)(float)(0.5 - 0.5 * cos(a));  // torch.hann_window(400) (periodic), f32 values
+  }
+  (void)two_pi_n;
+  // reflect-padded span: padded index p = f0*HOP + i  ->  original index j = p - 200
+  const int64_t base = (int64_t)f0 * HOP - N_FFT / 2;
+  for (int i = tid; i < SPAN; i += THREADS) {
+    int64_t j = base + i;
+    if (j < 0) j = -j;
+    if (j >= n_samples) j = 2 * (n_samples - 1) - j;
+    if (j < 0) j = 0;  // only for absurdly short inputs (guarded on the host)
+    xs[i] = x[j];
+  }
+  __syncthreads();
+
+  // |DFT|^2 for FT frames x 201 bins.  Thread -> (frame, bin) pairs, bin fastest.
+  const int n_frames_here = min(FT, n_out + 1 - f0);  // frames computed (last global frame dropped below)
+  for (int pidx = tid; pidx < FT * N_BINS; pidx += THREADS) {
+    const int f = pidx / N_BINS;
+    const int k = pidx - f * N_BINS;
+    double re = 0.0, im = 0.0;
+    if (f < n_frames_here) {
+      const float* xf = xs + f * HOP;
+      int idx = 0;
+#pragma unroll 8
+      for (int n = 0; n < N_FFT; ++n) {
+        const double v = (double)xf[n] * win[n];
+        re = fma(v, cosw[idx], re);
+        im = fma(v, sinw[idx], im);
+        idx += k;
+        if (idx >= N_FFT) idx -= N_FFT;
+      }
+    }
+    pw[f][k] = (float)(re * re + im * im);
+  }
+  __syncthreads();
+
+  // mel projection + log10; thread -> (mel, frame), frame fastest (time-contiguous stores)
+  float local_max = -INFINITY;
+  for (int o = tid; o < FT * n_mels; o += THREADS) {
+    const int m = o / FT;
+    const int f = o - m * FT;
+    const int t = f0 + f;
+    if (t >= n_out) continue;
+    float acc = 0.f;
+    for (int k = 0; k < N_BINS; ++k) acc = fmaf(fb[k * n_mels + m], pw[f][k], acc);
+    const float lg = log10f(fmaxf(acc, 1e-10f));
+    out[((int64_t)b * n_mels + m) * n_out + t] = lg;
+    local_max = fmaxf(local_max, lg);
+  }
+  local_max = wave_max(local_max);
+  if ((tid & 63) == 0) red[tid >> 6] = f2key(local_max);
+  __syncthreads();
+  if (tid == 0) {
+    uint32_t k = red[0];
+    for (int i = 1; i < THREADS / 64; ++i) k = max(k, red[i]);
+    atomicMax(clip_max + b, k);
+  }
+}
+
+__global__ void logmel_norm_kernel(float* __restrict__ out, int64_t per_clip, const uint32_t* __restrict__ clip_max) {
+  const int b = blockIdx.y;
+  const float mx = key2f(clip_max[b]) - 8.0f;
+  float* o = out + (int64_t)b * per_clip;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < per_clip; i += (int64_t)gridDim.x * blockDim.x) {
+    o[i] = (fmaxf(o[i], mx) + 4.0f) / 4.0f;
+  }
+}
+
+}  // namespace
+
+extern "C" int kw_log_mel(const float* audio, int64_t batch, int64_t n_samples, int64_t audio_stride,
+                          const float* mel_filters, int n_mels, float* out, void* workspace, kw_stream_t stream) {
+  if (!audio || !mel_filters || !out || !workspace || batch <= 0 || n_mels <= 0 || n_mels > 512)
+    return kw_set_error_msg(KW_EINVAL, "kw_log_mel: invalid arguments");
+  if (n_samples < N_FFT || n_samples % HOP != 0 || audio_stride < n_samples)
+    return kw_set_error_msg(KW_EINVAL, "kw_log_mel: n_samples must be >= 400, a multiple of 160, <= audio_stride");
+  hipStream_t s = (hipStream_t)stream;
+  const int n_out = (int)(n_samples / HOP);  // frames after dropping the last one
+  hipError_t e = hipMemsetAsync(workspace, 0, sizeof(uint32_t) * batch, s);
+  if (e != hipSuccess) return kw_set_error(e);
+  dim3 grid((n_out + FT - 1) / FT, (unsigned)batch);
+  hipLaunchKernelGGL(logmel_kernel, grid, dim3(THREADS), 0, s, audio, n_samples, audio_stride, mel_filters, n_mels,
+                     out, n_out, (uint32_t*)workspace);
+  KW_CHECK_LAUNCH();
+  hipLaunchKernelGGL(logmel_norm_kernel, dim3(64, (unsigned)batch), dim3(256), 0, s, out, (int64_t)n_mels * n_out,
+                     (const uint32_t*)workspace);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}

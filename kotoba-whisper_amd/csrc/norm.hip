@@ -1,0 +1,146 @@
+// LayerNorm, conv-stem re-layout and decoder embedding (HBM-bound row kernels).
+#include "kw_common.h"
+
+namespace {
+
+// ---- LayerNorm: one wave per row, row held in registers (two-pass mean/var), 16-B loads. ----------
+// TF/models/whisper/modeling_whisper.py:371,377,434,443,446,642,790 (nn.LayerNorm, eps 1e-5).
+constexpr int LN_MAXV = 8;  // float4 per lane -> dim <= 64*4*8 = 2048
+
+template <typename TOut>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t rows, int dim,
+                                                        const float* __restrict__ g, const float* __restrict__ bta,
+                                                        float eps, TOut* __restrict__ y) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float4* xr = reinterpret_cast<const float4*>(x + row * dim);
+  const int nv = dim >> 2;
+  float4 v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nv) {
+      v[i] = xr[c];
+      s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+    } else {
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
+  const float mean = wave_sum(s) / (float)dim;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nv) {
+      const float a = v[i].x - mean, b = v[i].y - mean, cc = v[i].z - mean, d = v[i].w - mean;
+      q += (a * a + b * b) + (cc * cc + d * d);
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)dim + eps);
+  TOut* yr = y + row * dim;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  const float4* b4 = reinterpret_cast<const float4*>(bta);
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nv) {
+      const float4 gg = g4[c], bb = b4[c];
+      float o0 = (v[i].x - mean) * rstd * gg.x + bb.x;
+      float o1 = (v[i].y - mean) * rstd * gg.y + bb.y;
+      float o2 = (v[i].z - mean) * rstd * gg.z + bb.z;
+      float o3 = (v[i].w - mean) * rstd * gg.w + bb.w;
+      if constexpr (sizeof(TOut) == 4) {
+        reinterpret_cast<float4*>(yr)[c] = make_float4(o0, o1, o2, o3);
+      } else {
+        ushort4 o;
+        o.x = f2bf(o0); o.y = f2bf(o1); o.z = f2bf(o2); o.w = f2bf(o3);
+        reinterpret_cast<ushort4*>(yr)[c] = o;
+      }
+    }
+  }
+}
+
+// ---- mel [B][C][T] f32 -> [B][T+2][c_pad] (zero time padding rows and zero channel padding) ----
+template <typename TOut>
+__global__ __launch_bounds__(256) void mel_tm_kernel(const float* __restrict__ mel, int C, int T, int c_pad,
+                                                     TOut* __restrict__ out) {
+  __shared__ float tile[32][33];
+  const int b = blockIdx.z;
+  const int t0 = blockIdx.x * 32;  // output time row block (padded coordinates)
+  const int c0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (int i = ty; i < 32; i += 8) {
+    const int c = c0 + i, tp = t0 + tx;  // read mel[b][c][tp-1]
+    float v = 0.f;
+    if (c < C && tp >= 1 && tp <= T) v = mel[((int64_t)b * C + c) * T + (tp - 1)];
+    tile[i][tx] = v;
+  }
+  __syncthreads();
+  for (int i = ty; i < 32; i += 8) {
+    const int tp = t0 + i, c = c0 + tx;
+    if (tp < T + 2 && c < c_pad) TypeIO<TOut>::st(out + ((int64_t)b * (T + 2) + tp) * c_pad + c, tile[tx][i]);
+  }
+}
+
+// ---- decoder embedding: h = tok_emb[id] + pos_emb[pos] (f32 residual stream) ----------------------
+template <typename TW>
+__global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, int64_t ids_stride, int q_len,
+                                                    const int32_t* __restrict__ cur_len, const TW* __restrict__ tok,
+                                                    const TW* __restrict__ pos, int d, float* __restrict__ h) {
+  const int r = blockIdx.x;  // b*q_len + i
+  const int b = r / q_len, i = r - b * q_len;
+  const int p = *cur_len - q_len + i;
+  const int64_t id = ids[(int64_t)b * ids_stride + p];
+  for (int c = threadIdx.x; c < d; c += blockDim.x)
+    h[(int64_t)r * d + c] = TypeIO<TW>::ld(tok + id * d + c) + TypeIO<TW>::ld(pos + (int64_t)p * d + c);
+}
+
+}  // namespace
+
+extern "C" int kw_layernorm(const float* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
+                            float eps, void* y, int y_dtype, kw_stream_t stream) {
+  if (!x || !gamma || !beta || !y || rows < 0 || dim <= 0 || dim % 4 != 0 || dim > 64 * 4 * LN_MAXV)
+    return kw_set_error_msg(KW_EINVAL, "kw_layernorm: invalid arguments (dim % 4 == 0, dim <= 2048)");
+  if (rows == 0) return KW_OK;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  if (y_dtype == KW_DT_F32)
+    hipLaunchKernelGGL(layernorm_kernel<float>, grid, dim3(256), 0, s, x, rows, (int)dim, gamma, beta, eps, (float*)y);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<bf16_t>, grid, dim3(256), 0, s, x, rows, (int)dim, gamma, beta, eps, (bf16_t*)y);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}
+
+extern "C" int kw_mel_to_time_major(const float* mel, int64_t B, int64_t C, int64_t T, int64_t c_pad, void* out,
+                                    int out_dtype, kw_stream_t stream) {
+  if (!mel || !out || B <= 0 || C <= 0 || T <= 0 || c_pad < C)
+    return kw_set_error_msg(KW_EINVAL, "kw_mel_to_time_major: invalid arguments");
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((T + 2 + 31) / 32), (unsigned)((c_pad + 31) / 32), (unsigned)B);
+  if (out_dtype == KW_DT_F32)
+    hipLaunchKernelGGL(mel_tm_kernel<float>, grid, dim3(256), 0, s, mel, (int)C, (int)T, (int)c_pad, (float*)out);
+  else
+    hipLaunchKernelGGL(mel_tm_kernel<bf16_t>, grid, dim3(256), 0, s, mel, (int)C, (int)T, (int)c_pad, (bf16_t*)out);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}
+
+extern "C" int kw_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
+                        const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
+                        kw_stream_t stream) {
+  if (!ids || !cur_len || !tok_emb || !pos_emb || !h || B <= 0 || q_len <= 0 || d <= 0)
+    return kw_set_error_msg(KW_EINVAL, "kw_embed: invalid arguments");
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)(B * q_len));
+  if (dtype == KW_DT_F32)
+    hipLaunchKernelGGL(embed_kernel<float>, grid, dim3(256), 0, s, ids, ids_stride, (int)q_len, cur_len,
+                       (const float*)tok_emb, (const float*)pos_emb, (int)d, h);
+  else
+    hipLaunchKernelGGL(embed_kernel<bf16_t>, grid, dim3(256), 0, s, ids, ids_stride, (int)q_len, cur_len,
+                       (const bf16_t*)tok_emb, (const bf16_t*)pos_emb, (int)d, h);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}

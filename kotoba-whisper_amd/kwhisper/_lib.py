@@ -1,0 +1,105 @@
+"""ctypes binding of the kwhisper C ABI (include/kwhisper.h).
+
+The shared library is built in-tree (``kotoba-whisper_amd/csrc/Makefile`` ->
+``kwhisper/libkwhisper.so``).  There is no fallback: if the library is
+missing or fails to load, every op raises.  torch is imported first so the
+library binds to the HIP runtime torch already loaded (one runtime per
+process; both carry SONAME libamdhip64.so.7).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkwhisper.so")
+
+KW_OK, KW_EINVAL, KW_EHIP, KW_EUNSUPPORTED = 0, 1, 2, 3
+KW_DT_F32, KW_DT_BF16 = 0, 1
+KW_EPI_STORE, KW_EPI_RESID, KW_EPI_HEADSPLIT = 0, 1, 2
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_vp = ctypes.c_void_p
+
+
+class GemmArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int), ("c_dtype", ctypes.c_int),
+        ("A", c_vp), ("lda", c_i64), ("a_rows_per_batch", c_i64), ("a_batch_stride", c_i64),
+        ("W", c_vp), ("bias", c_vp),
+        ("C", c_vp), ("ldc", c_i64), ("c_rows_per_batch", c_i64), ("c_batch_stride", c_i64),
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
+        ("epilogue", ctypes.c_int), ("gelu", ctypes.c_int),
+        ("scale", ctypes.c_float), ("scale_cols", c_i64),
+        ("row_add", c_vp), ("row_add_period", c_i64),
+        ("hs_seq", c_i64), ("hs_heads", c_i64), ("hs_head_dim", c_i64),
+    ]
+
+
+class SamplerArgs(ctypes.Structure):
+    _fields_ = [
+        ("logits", c_vp), ("B", c_i64), ("V", c_i64),
+        ("suppress_mask", c_vp), ("begin_suppress", c_vp), ("n_begin_suppress", c_i32),
+        ("return_timestamps", c_i32),
+        ("ts_begin", c_i32), ("no_ts_id", c_i32), ("eos_id", c_i32), ("pad_id", c_i32),
+        ("max_initial_ts", c_i32),
+        ("ids", c_vp), ("ids_stride", c_i64),
+        ("cur_len", c_vp), ("max_length", c_i32), ("begin_index", c_i32),
+        ("unfinished", c_vp), ("counter", c_vp), ("n_unfinished", c_vp), ("scores_out", c_vp),
+    ]
+
+
+EXPORTS = {
+    "kw_version": (ctypes.c_int, []),
+    "kw_last_error": (ctypes.c_char_p, []),
+    "kw_log_mel": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp, c_vp, c_vp]),
+    "kw_mel_to_time_major": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp]),
+    "kw_gemm": (ctypes.c_int, [ctypes.POINTER(GemmArgs), c_vp]),
+    "kw_gemv": (ctypes.c_int, [ctypes.POINTER(GemmArgs), c_vp]),
+    "kw_pack_weight": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
+    "kw_packed_weight_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
+    "kw_layernorm": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp]),
+    "kw_attention": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
+    "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "kw_self_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                         c_vp, c_vp]),
+    "kw_cross_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
+                                          c_vp, ctypes.c_size_t, c_vp]),
+    "kw_cross_attn_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64, c_i64]),
+    "kw_greedy_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), c_vp]),
+}
+
+_lib = None
+
+
+class KWError(RuntimeError):
+    pass
+
+
+def load(path: str = LIB_PATH):
+    """Load and type the library once; raises if it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise KWError(
+            f"kwhisper native library not found at {path}; build it with "
+            "`make -C kotoba-whisper_amd/csrc` or `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in EXPORTS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != KW_OK:
+        msg = _lib.kw_last_error().decode(errors="replace") if _lib is not None else ""
+        if rc == KW_EINVAL:
+            raise ValueError(f"{what}: {msg}")
+        raise KWError(f"{what} failed (code {rc}): {msg}")

@@ -1,0 +1,247 @@
+"""Device-resident greedy decoding for one batch (WhisperDecoder + GenerationMixin._sample).
+
+A ``DecodeSession`` owns the static caches and step buffers of one batch:
+  * cross K/V of every layer ([2L][B][H][1500][64], one GEMM, TF modeling_whisper.py:323-335);
+  * self K/V static cache [L][B][H][448][64] (replaces DynamicLayer's torch.cat growth,
+    TF/cache_utils.py:127-145);
+  * ids [B][448] int64, cur_len, unfinished flags -- all on device, advanced by kw_greedy_step.
+The prefill (prompt of P tokens) runs eagerly; the single-token step (32 x 11 kernels + final LN +
+LM head + sampler) is captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed: the step
+reads its position from device memory, so one graph serves every step.  The host only polls the
+device unfinished-row count a few steps behind the GPU (no per-step sync).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import ops
+
+_HD = 64
+T_MAX = 448
+
+
+class DecodeSession:
+    def __init__(self, eng, B: int, enc: torch.Tensor | None = None):
+        s = eng.shape
+        self.eng, self.B = eng, B
+        dev, dt = eng.device, eng.dtype
+        d, H, Ld = s.d_model, eng.H, s.decoder_layers
+        self.T = s.max_source_positions
+        self.cross = torch.empty((2 * Ld, B, H, self.T, _HD), device=dev, dtype=dt)
+        self.kc = torch.zeros((Ld, B, H, T_MAX, _HD), device=dev, dtype=dt)
+        self.vc = torch.zeros((Ld, B, H, T_MAX, _HD), device=dev, dtype=dt)
+        self.ids = torch.zeros((B, T_MAX + 1), device=dev, dtype=torch.int64)
+        self.cur_len = torch.zeros((1,), device=dev, dtype=torch.int32)
+        self.unfinished = torch.ones((B,), device=dev, dtype=torch.int32)
+        self.counter = torch.zeros((1,), device=dev, dtype=torch.int32)
+        self.n_unfinished = torch.zeros((1,), device=dev, dtype=torch.int32)
+        self.logits = torch.empty((B, s.vocab_size), device=dev, dtype=torch.float32)
+        self._bufs = {}
+        self._plans = {}
+        self._graph = None
+        self._graph_key = None
+        if enc is not None:
+            self.set_encoder_output(enc)
+
+    # ------------------------------------------------------------------------------------------
+    def set_encoder_output(self, enc: torch.Tensor) -> None:
+        self.eng.cross_kv(enc, self.B, out=self.cross)
+
+    def _buffers(self, q: int):
+        if q not in self._bufs:
+            s, dev, dt = self.eng.shape, self.eng.device, self.eng.dtype
+            d, rows = s.d_model, self.B * q
+            self._bufs[q] = dict(
+                h=torch.empty((rows, d), device=dev, dtype=torch.float32),
+                x=torch.empty((rows, d), device=dev, dtype=dt),
+                qkv=torch.empty((rows, 3 * d), device=dev, dtype=dt),
+                attn=torch.empty((rows, d), device=dev, dtype=dt),
+                qx=torch.empty((rows, d), device=dev, dtype=dt),
+                ffn=torch.empty((rows, s.decoder_ffn_dim), device=dev, dtype=dt),
+                ws=torch.empty((ops.cross_attn_workspace_bytes(self.B, q, self.eng.H, _HD, self.T) // 4 + 1,),
+                               device=dev, dtype=torch.float32),
+            )
+        return self._bufs[q]
+
+    def _gemm(self, A, W, C, M, N, K, **kw):
+        """Row-chunked skinny GEMM (kw_gemv handles M <= 128) or the f32 GEMM in parity mode."""
+        eng = self.eng
+        if not eng.packed:
+            return [ops.GemmPlan(A, W, C, M, N, K, **kw)]
+        plans = []
+        lda = kw.pop("lda", K)
+        ldc = kw.pop("ldc", N)
+        a_off = kw.pop("a_offset", 0)
+        for m0 in range(0, M, 128):
+            mm = min(128, M - m0)
+            plans.append(ops.GemmPlan(A, W, C, mm, N, K, lda=lda, ldc=ldc, a_offset=a_off + m0 * lda,
+                                      c_offset=m0 * ldc, packed=True, dtype=torch.bfloat16, **kw))
+        return plans
+
+    def _step_plans(self, q: int):
+        """The decoder forward for q new positions per row (q = prompt length for the prefill, 1 after)."""
+        if q in self._plans:
+            return self._plans[q]
+        eng, s = self.eng, self.eng.shape
+        b = self._buffers(q)
+        d, H, B = s.d_model, eng.H, self.B
+        rows = B * q
+        scale = _HD ** -0.5
+        eps = s.layer_norm_eps
+        seq = [("embed", q, b["h"])]
+        for li, lay in enumerate(eng.dec_layers):
+            seq.append(("ln", b["h"], lay["ln1_g"], lay["ln1_b"], b["x"]))
+            seq += self._gemm(b["x"], lay["qkv_w"], b["qkv"], rows, 3 * d, d, bias=lay["qkv_b"], scale=scale, scale_cols=d)
+            seq.append(("self", q, b["qkv"], li, b["attn"]))
+            seq += self._gemm(b["attn"], lay["o_w"], b["h"], rows, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID)
+            seq.append(("ln", b["h"], lay["ln2_g"], lay["ln2_b"], b["x"]))
+            seq += self._gemm(b["x"], lay["xq_w"], b["qx"], rows, d, d, bias=lay["xq_b"], scale=scale, scale_cols=d)
+            seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
+            seq += self._gemm(b["attn"], lay["xo_w"], b["h"], rows, d, d, bias=lay["xo_b"], epilogue=L.KW_EPI_RESID)
+            seq.append(("ln", b["h"], lay["ln3_g"], lay["ln3_b"], b["x"]))
+            seq += self._gemm(b["x"], lay["fc1_w"], b["ffn"], rows, s.decoder_ffn_dim, d, bias=lay["fc1_b"], gelu=True)
+            seq += self._gemm(b["ffn"], lay["fc2_w"], b["h"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
+                              epilogue=L.KW_EPI_RESID)
+        seq.append(("ln", b["h"], eng.dec_ln_g, eng.dec_ln_b, b["x"]))
+        # LM head on the last position of every row (proj_out tied to embed_tokens, f32 logits)
+        seq += self._gemm(b["x"], eng.lm_w, self.logits, B, s.vocab_size, d, lda=q * d, a_offset=(q - 1) * d)
+        self._plans[q] = seq
+        return seq
+
+    def _run(self, seq):
+        eng, s = self.eng, self.eng.shape
+        H, B = eng.H, self.B
+        for p in seq:
+            if not isinstance(p, tuple):
+                p()
+                continue
+            k = p[0]
+            if k == "ln":
+                ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4])
+            elif k == "embed":
+                ops.embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2])
+            elif k == "self":
+                _, q, qkv, li, out = p
+                ops.self_attn_step(qkv, B, q, H, _HD, self.kc[li], self.vc[li], T_MAX, self.cur_len, out)
+            elif k == "cross":
+                _, q, qx, li, out, ws = p
+                ops.cross_attn_step(qx, B, q, H, _HD, self.cross[2 * li], self.cross[2 * li + 1], self.T, out, ws)
+
+    # ------------------------------------------------------------------------------------------
+    def forward_logits(self, prompt: torch.Tensor) -> torch.Tensor:
+        """Prefill only: logits (B, V) for the last prompt position (detect_language)."""
+        P = prompt.shape[1]
+        self.ids[:, :P].copy_(prompt)
+        self.cur_len.fill_(P)
+        self._run(self._step_plans(P))
+        return self.logits
+
+    def teacher_forced_logits(self, seq: torch.Tensor, P: int) -> torch.Tensor:
+        """Raw logits (B, T-P+1, V) predicting seq[:, P:] and one more, feeding the reference tokens
+        (validation utility: compares the decoder step with a reference's per-step logits)."""
+        B, T = seq.shape
+        seq = seq.to(self.eng.device)
+        self.ids.zero_()
+        self.ids[:, :T].copy_(seq)
+        self.cur_len.fill_(P)
+        out = []
+        self._run(self._step_plans(P))
+        out.append(self.logits.clone())
+        step = self._step_plans(1)
+        for t in range(P, T):
+            self.cur_len.fill_(t + 1)
+            self._run(step)
+            out.append(self.logits.clone())
+        return torch.stack(out, 1)
+
+    def generate(self, prompt: torch.Tensor, gen, *, max_length: int, return_timestamps: bool,
+                 check_every: int = 4, use_graph: bool = True, record_scores: bool = False):
+        """Greedy loop of GenerationMixin._sample (TF/generation/utils.py:2783-2941).
+
+        Returns host int64 ids (B, L) including the prompt, with L exactly the length the reference
+        loop stops at (all rows finished or max_length)."""
+        B = self.B
+        P = prompt.shape[1]
+        if P + 1 > T_MAX + 1 or max_length > T_MAX:
+            raise ValueError(f"max_length {max_length} exceeds max_target_positions {T_MAX}")
+        dev = self.eng.device
+        self.ids.zero_()
+        self.ids[:, :P].copy_(prompt.to(dev))
+        self.cur_len.fill_(P)
+        self.unfinished.fill_(1)
+        self.counter.zero_()
+        self.n_unfinished.fill_(B)
+        sup = torch.zeros((self.eng.shape.vocab_size,), dtype=torch.uint8)
+        if gen.suppress_tokens:
+            sup[torch.tensor(gen.suppress_tokens)] = 1
+        self._sup = sup.to(dev)
+        self._bsup = torch.tensor(gen.begin_suppress_tokens or [0], dtype=torch.int32, device=dev)
+        nb = len(gen.begin_suppress_tokens or [])
+        self.scores = [] if record_scores else None
+        score_buf = torch.empty_like(self.logits) if record_scores else None
+        sampler = ops.SamplerPlan(self.logits, self._sup, self._bsup if nb else None, self.ids, self.cur_len,
+                                  self.unfinished, self.counter, self.n_unfinished,
+                                  return_timestamps=return_timestamps, ts_begin=gen.timestamp_begin,
+                                  no_ts_id=gen.no_timestamps_token_id, eos_id=gen.eos_token_id,
+                                  pad_id=gen.pad_token_id, max_initial_ts=gen.max_initial_timestamp_index,
+                                  max_length=max_length, begin_index=P, scores_out=score_buf)
+        # prefill
+        self._run(self._step_plans(P))
+        sampler()
+        if record_scores:
+            self.scores.append((self.logits.clone(), score_buf.clone()))
+        n_steps = max_length - P  # tokens the reference can add at most
+        done = 1
+        step_seq = self._step_plans(1)
+
+        def one_step():
+            self._run(step_seq)
+            sampler()
+
+        graph = None
+        if use_graph and not record_scores and n_steps > 1:
+            key = (max_length, P, return_timestamps, id(sampler))
+            graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.graph(graph, stream=side):
+                one_step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            self._graph, self._graph_key = graph, key
+        pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
+        events = []
+        while done < n_steps:
+            if graph is not None:
+                graph.replay()
+            else:
+                one_step()
+            if record_scores:
+                self.scores.append((self.logits.clone(), score_buf.clone()))
+            done += 1
+            slot = done % (check_every + 1)
+            pinned[slot : slot + 1].copy_(self.n_unfinished, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            events.append((ev, slot))
+            if len(events) > check_every:
+                e0, s0 = events.pop(0)
+                e0.synchronize()
+                if int(pinned[s0]) == 0:
+                    break
+        torch.cuda.synchronize(dev)
+        L_now = int(self.cur_len.item())
+        ids = self.ids[:, :L_now].cpu().numpy()
+        return _reference_length(ids, P, gen.eos_token_id, max_length)
+
+
+def _reference_length(ids: np.ndarray, P: int, eos: int, max_length: int) -> np.ndarray:
+    """Trim to the length at which the reference's while-loop would have stopped."""
+    B, L_now = ids.shape
+    stop = []
+    for b in range(B):
+        hit = np.nonzero(ids[b, P:] == eos)[0]
+        stop.append(P + int(hit[0]) + 1 if hit.size else max_length)
+    L_ref = min(max(stop), max_length, L_now)
+    return ids[:, :L_ref]

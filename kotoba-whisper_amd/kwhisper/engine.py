@@ -1,0 +1,234 @@
+"""WhisperEngine: weights in HBM, the encoder pass and device-resident decode sessions.
+
+Mirrors the compute of ``WhisperForConditionalGeneration`` (TF/models/whisper/modeling_whisper.py):
+encoder :592-646, decoder :690-795, proj_out :1080.  Every op is a kwhisper HIP kernel through the
+C ABI; torch only owns memory, streams and graph capture.
+
+Layout in HBM (DESIGN.md §Data layout):
+  * residual stream f32 [rows][d]; GEMM inputs (LayerNorm outputs) in the compute dtype;
+  * conv stem: mel -> time-major zero-padded [B][3002][c_pad], conv1 output [B][3002][d]
+    (pad rows stay zero), so both convolutions are im2col-free GEMMs;
+  * encoder q/k/v head-split [3][B][H][1500][64]; cross-attention K/V of all decoder layers from ONE
+    GEMM straight into the static cache [2L][B][H][1500][64];
+  * decoder self K/V static cache [L][B][H][448][64]; decode-step weights pre-packed into 1-KB MFMA
+    fragments (bf16) for the skinny GEMMs.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import ops
+from .config import GenerationConstants, WhisperShape, generation_constants
+
+_HD = 64
+
+
+def _to_tensor(v) -> torch.Tensor:
+    if isinstance(v, torch.Tensor):
+        return v.detach().float()
+    return torch.from_numpy(np.asarray(v, dtype=np.float32))
+
+
+class _EncoderBuffers:
+    def __init__(self, eng: "WhisperEngine", B: int):
+        s, dev, dt = eng.shape, eng.device, eng.dtype
+        d, T = s.d_model, s.max_source_positions
+        self.B = B
+        self.mel_tm = torch.empty((B, s.n_frames + 2, eng.c_pad), device=dev, dtype=dt)
+        self.conv = torch.zeros((B, s.n_frames + 2, d), device=dev, dtype=dt)  # pad rows stay zero
+        self.h = torch.empty((B * T, d), device=dev, dtype=torch.float32)
+        self.x = torch.empty((B * T, d), device=dev, dtype=dt)
+        self.qkv = torch.empty((3 * B * T * d,), device=dev, dtype=dt)
+        self.attn = torch.empty((B * T, d), device=dev, dtype=dt)
+        self.ffn = torch.empty((B * T, s.encoder_ffn_dim), device=dev, dtype=dt)
+        self.out = torch.empty((B * T, d), device=dev, dtype=dt)
+        self.plans = eng._encoder_plans(self)
+
+
+class WhisperEngine:
+    """The MI355X Whisper model: ``encode`` (mel -> hidden) and decode sessions.
+
+    ``dtype`` = torch.bfloat16 (performance path, bf16 MFMA, f32 accumulation and residual) or
+    torch.float32 (parity path: exact-fp32 MFMA; greedy tokens match the fp32 reference).
+    """
+
+    def __init__(self, shape: WhisperShape, state_dict: dict, *, dtype=torch.bfloat16, device="cuda",
+                 generation_config: GenerationConstants | None = None):
+        if dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("dtype must be torch.bfloat16 or torch.float32")
+        L.load()
+        self.shape = shape
+        self.dtype = dtype
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise ValueError("WhisperEngine runs on a cuda (HIP) device only")
+        self.generation_config = generation_config or generation_constants(shape)
+        d = shape.d_model
+        self.H = shape.encoder_attention_heads
+        if d // self.H != _HD:
+            raise ValueError("head_dim must be 64")
+        self.c_pad = (-(-shape.num_mel_bins // 64) * 64) if dtype == torch.bfloat16 else (-(-shape.num_mel_bins // 16) * 16)
+        self._load(state_dict)
+        self._enc = {}
+
+    # ------------------------------------------------------------------------------------------
+    def _dev(self, t: torch.Tensor, dtype=None) -> torch.Tensor:
+        return t.to(device=self.device, dtype=dtype or self.dtype).contiguous()
+
+    def _load(self, sd: dict) -> None:
+        s = self.shape
+        d = s.d_model
+        g = lambda n: _to_tensor(sd[n])  # noqa: E731
+        f32 = torch.float32
+        # conv stem as GEMMs: W'[o][k*C + c] = W[o][c][k]
+        w1 = g("model.encoder.conv1.weight")  # (d, n_mels, 3)
+        w1p = torch.zeros((d, 3, self.c_pad), device=w1.device)
+        w1p[:, :, : s.num_mel_bins] = w1.permute(0, 2, 1)
+        self.conv1_w = self._dev(w1p.reshape(d, 3 * self.c_pad))
+        self.conv1_b = self._dev(g("model.encoder.conv1.bias"), f32)
+        self.conv2_w = self._dev(g("model.encoder.conv2.weight").permute(0, 2, 1).reshape(d, 3 * d))
+        self.conv2_b = self._dev(g("model.encoder.conv2.bias"), f32)
+        self.enc_pos = self._dev(g("model.encoder.embed_positions.weight"), f32)
+        zero = torch.zeros(d, device=w1.device)
+
+        def attn_qkv(p):
+            w = torch.cat([g(f"{p}.q_proj.weight"), g(f"{p}.k_proj.weight"), g(f"{p}.v_proj.weight")], 0)
+            b = torch.cat([g(f"{p}.q_proj.bias"), zero, g(f"{p}.v_proj.bias")], 0)
+            return w, b
+
+        self.enc_layers = []
+        for i in range(s.encoder_layers):
+            p = f"model.encoder.layers.{i}"
+            qkv_w, qkv_b = attn_qkv(f"{p}.self_attn")
+            self.enc_layers.append(dict(
+                ln1_g=self._dev(g(f"{p}.self_attn_layer_norm.weight"), f32),
+                ln1_b=self._dev(g(f"{p}.self_attn_layer_norm.bias"), f32),
+                qkv_w=self._dev(qkv_w), qkv_b=self._dev(qkv_b, f32),
+                o_w=self._dev(g(f"{p}.self_attn.out_proj.weight")), o_b=self._dev(g(f"{p}.self_attn.out_proj.bias"), f32),
+                ln2_g=self._dev(g(f"{p}.final_layer_norm.weight"), f32),
+                ln2_b=self._dev(g(f"{p}.final_layer_norm.bias"), f32),
+                fc1_w=self._dev(g(f"{p}.fc1.weight")), fc1_b=self._dev(g(f"{p}.fc1.bias"), f32),
+                fc2_w=self._dev(g(f"{p}.fc2.weight")), fc2_b=self._dev(g(f"{p}.fc2.bias"), f32),
+            ))
+        self.enc_ln_g = self._dev(g("model.encoder.layer_norm.weight"), f32)
+        self.enc_ln_b = self._dev(g("model.encoder.layer_norm.bias"), f32)
+
+        # decoder
+        self.tok_emb = self._dev(g("model.decoder.embed_tokens.weight"))
+        self.dec_pos = self._dev(g("model.decoder.embed_positions.weight"))
+        packed = self.dtype == torch.bfloat16
+        self.packed = packed
+        pk = ops.pack_weight if packed else (lambda w: w)
+        self.dec_layers = []
+        ckv_w, ckv_b = [], []
+        for i in range(s.decoder_layers):
+            p = f"model.decoder.layers.{i}"
+            qkv_w, qkv_b = attn_qkv(f"{p}.self_attn")
+            lay = dict(
+                ln1_g=self._dev(g(f"{p}.self_attn_layer_norm.weight"), f32),
+                ln1_b=self._dev(g(f"{p}.self_attn_layer_norm.bias"), f32),
+                qkv_w=pk(self._dev(qkv_w)), qkv_b=self._dev(qkv_b, f32),
+                o_w=pk(self._dev(g(f"{p}.self_attn.out_proj.weight"))),
+                o_b=self._dev(g(f"{p}.self_attn.out_proj.bias"), f32),
+                ln2_g=self._dev(g(f"{p}.encoder_attn_layer_norm.weight"), f32),
+                ln2_b=self._dev(g(f"{p}.encoder_attn_layer_norm.bias"), f32),
+                xq_w=pk(self._dev(g(f"{p}.encoder_attn.q_proj.weight"))),
+                xq_b=self._dev(g(f"{p}.encoder_attn.q_proj.bias"), f32),
+                xo_w=pk(self._dev(g(f"{p}.encoder_attn.out_proj.weight"))),
+                xo_b=self._dev(g(f"{p}.encoder_attn.out_proj.bias"), f32),
+                ln3_g=self._dev(g(f"{p}.final_layer_norm.weight"), f32),
+                ln3_b=self._dev(g(f"{p}.final_layer_norm.bias"), f32),
+                fc1_w=pk(self._dev(g(f"{p}.fc1.weight"))), fc1_b=self._dev(g(f"{p}.fc1.bias"), f32),
+                fc2_w=pk(self._dev(g(f"{p}.fc2.weight"))), fc2_b=self._dev(g(f"{p}.fc2.bias"), f32),
+            )
+            self.dec_layers.append(lay)
+            ckv_w += [g(f"{p}.encoder_attn.k_proj.weight"), g(f"{p}.encoder_attn.v_proj.weight")]
+            ckv_b += [zero, g(f"{p}.encoder_attn.v_proj.bias")]
+        self.cross_kv_w = self._dev(torch.cat(ckv_w, 0))
+        self.cross_kv_b = self._dev(torch.cat(ckv_b, 0), f32)
+        self.dec_ln_g = self._dev(g("model.decoder.layer_norm.weight"), f32)
+        self.dec_ln_b = self._dev(g("model.decoder.layer_norm.bias"), f32)
+        self.lm_w = pk(self.tok_emb) if packed else self.tok_emb
+        torch.cuda.synchronize(self.device)
+
+    # ------------------------------------------------------------------------------------------
+    # encoder
+    # ------------------------------------------------------------------------------------------
+    def _encoder_plans(self, bf: _EncoderBuffers):
+        s, B, d = self.shape, bf.B, self.shape.d_model
+        T, F = s.max_source_positions, s.n_frames
+        M = B * T
+        eps = s.layer_norm_eps
+        plans = []
+        plans.append(ops.GemmPlan(bf.mel_tm, self.conv1_w, bf.conv, B * F, d, 3 * self.c_pad, bias=self.conv1_b,
+                                  lda=self.c_pad, a_rows_per_batch=F, a_batch_stride=(F + 2) * self.c_pad,
+                                  ldc=d, c_rows_per_batch=F, c_batch_stride=(F + 2) * d, c_offset=d, gelu=True))
+        plans.append(ops.GemmPlan(bf.conv, self.conv2_w, bf.h, M, d, 3 * d, bias=self.conv2_b,
+                                  lda=2 * d, a_rows_per_batch=T, a_batch_stride=(F + 2) * d,
+                                  gelu=True, row_add=self.enc_pos, row_add_period=T))
+        scale = _HD ** -0.5
+        for lay in self.enc_layers:
+            plans.append(("ln", bf.h, lay["ln1_g"], lay["ln1_b"], bf.x))
+            plans.append(ops.GemmPlan(bf.x, lay["qkv_w"], bf.qkv, M, 3 * d, d, bias=lay["qkv_b"],
+                                      epilogue=L.KW_EPI_HEADSPLIT, scale=scale, scale_cols=d,
+                                      hs_seq=T, hs_heads=self.H, hs_head_dim=_HD))
+            plans.append(("attn", bf.qkv, bf.attn))
+            plans.append(ops.GemmPlan(bf.attn, lay["o_w"], bf.h, M, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID))
+            plans.append(("ln", bf.h, lay["ln2_g"], lay["ln2_b"], bf.x))
+            plans.append(ops.GemmPlan(bf.x, lay["fc1_w"], bf.ffn, M, s.encoder_ffn_dim, d, bias=lay["fc1_b"], gelu=True))
+            plans.append(ops.GemmPlan(bf.ffn, lay["fc2_w"], bf.h, M, d, s.encoder_ffn_dim, bias=lay["fc2_b"],
+                                      epilogue=L.KW_EPI_RESID))
+        plans.append(("ln", bf.h, self.enc_ln_g, self.enc_ln_b, bf.out))
+        return plans
+
+    def encoder_buffers(self, B: int) -> _EncoderBuffers:
+        if B not in self._enc:
+            self._enc[B] = _EncoderBuffers(self, B)
+        return self._enc[B]
+
+    def encode(self, mel: torch.Tensor) -> torch.Tensor:
+        """mel (B, n_mels, 3000) -> encoder last_hidden_state as (B*1500, d) in the compute dtype.
+
+        Mirrors WhisperEncoder.forward (modeling_whisper.py:592-646), including its frame check.
+        """
+        s = self.shape
+        if mel.dim() != 3 or mel.shape[1] != s.num_mel_bins:
+            raise ValueError(f"input_features must be (batch, {s.num_mel_bins}, frames)")
+        if mel.shape[-1] != s.n_frames:
+            raise ValueError(
+                f"Whisper expects the mel input features to be of length {s.n_frames}, but found {mel.shape[-1]}. "
+                f"Make sure to pad the input mel features to {s.n_frames}."
+            )
+        mel = mel.to(device=self.device, dtype=torch.float32).contiguous()
+        B = mel.shape[0]
+        bf = self.encoder_buffers(B)
+        ops.mel_to_time_major(mel, self.c_pad, self.dtype, out=bf.mel_tm)
+        T = s.max_source_positions
+        for p in bf.plans:
+            if isinstance(p, tuple):
+                if p[0] == "ln":
+                    ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4])
+                else:
+                    ops.attention(p[1], B, self.H, T, _HD, p[2])
+            else:
+                p()
+        return bf.out
+
+    # ------------------------------------------------------------------------------------------
+    def cross_kv(self, enc: torch.Tensor, B: int, out: torch.Tensor | None = None) -> torch.Tensor:
+        """All decoder layers' cross-attention K/V in one GEMM: [2L][B][H][1500][64] (modeling_whisper.py:323-335)."""
+        s = self.shape
+        T, d = s.max_source_positions, s.d_model
+        n = 2 * s.decoder_layers * d
+        if out is None:
+            out = torch.empty((2 * s.decoder_layers, B, self.H, T, _HD), device=self.device, dtype=self.dtype)
+        ops.GemmPlan(enc, self.cross_kv_w, out, B * T, n, d, bias=self.cross_kv_b, epilogue=L.KW_EPI_HEADSPLIT,
+                     hs_seq=T, hs_heads=self.H, hs_head_dim=_HD)()
+        return out
+
+    def new_session(self, B: int, enc: torch.Tensor | None = None) -> "DecodeSession":
+        from .decode import DecodeSession
+
+        return DecodeSession(self, B, enc)

@@ -1,0 +1,201 @@
+"""Torch-tensor front end of the kwhisper C ABI.
+
+Each function validates shapes/dtypes/devices, then launches on the current
+torch stream.  Tensors are plumbing only (device memory + stream); all
+arithmetic happens in the HIP kernels of ``libkwhisper.so``.  ``GemmPlan`` /
+``GemvPlan`` pre-build the C argument block once so decode steps can be
+replayed (and hipGraph-captured) without Python-side re-validation.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+_DT = {torch.float32: L.KW_DT_F32, torch.bfloat16: L.KW_DT_BF16}
+
+
+def _lib():
+    return L.load()
+
+
+def _p(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _s():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _dt(t: torch.Tensor) -> int:
+    try:
+        return _DT[t.dtype]
+    except KeyError:
+        raise ValueError(f"unsupported dtype {t.dtype}; expected float32 or bfloat16") from None
+
+
+def _cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("kwhisper ops take device (cuda) tensors")
+
+
+def log_mel(audio: torch.Tensor, mel_filters: torch.Tensor, out: torch.Tensor | None = None,
+            workspace: torch.Tensor | None = None) -> torch.Tensor:
+    """audio (B, n) f32, n % 160 == 0 -> (B, n_mels, n // 160) f32 log-mel."""
+    _cuda(audio, mel_filters)
+    if audio.dim() != 2 or audio.dtype != torch.float32 or audio.stride(1) != 1:
+        raise ValueError("audio must be a (B, n_samples) float32 tensor with unit inner stride")
+    if mel_filters.dim() != 2 or mel_filters.shape[0] != 201 or not mel_filters.is_contiguous():
+        raise ValueError("mel_filters must be a contiguous (201, n_mels) float32 tensor")
+    b, n = audio.shape
+    n_mels = mel_filters.shape[1]
+    if out is None:
+        out = torch.empty((b, n_mels, n // 160), device=audio.device, dtype=torch.float32)
+    if workspace is None:
+        workspace = torch.empty((max(b, 1),), device=audio.device, dtype=torch.int32)
+    L.check(_lib().kw_log_mel(_p(audio), b, n, audio.stride(0), _p(mel_filters), n_mels, _p(out), _p(workspace), _s()),
+            "kw_log_mel")
+    return out
+
+
+def mel_to_time_major(mel: torch.Tensor, c_pad: int, dtype: torch.dtype, out: torch.Tensor | None = None):
+    _cuda(mel)
+    b, c, t = mel.shape
+    if out is None:
+        out = torch.empty((b, t + 2, c_pad), device=mel.device, dtype=dtype)
+    L.check(_lib().kw_mel_to_time_major(_p(mel.contiguous()), b, c, t, c_pad, _p(out), _DT[dtype], _s()),
+            "kw_mel_to_time_major")
+    return out
+
+
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor):
+    _cuda(x, gamma, beta, out)
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("layernorm input must be contiguous float32")
+    dim = x.shape[-1]
+    rows = x.numel() // dim
+    L.check(_lib().kw_layernorm(_p(x), rows, dim, _p(gamma), _p(beta), eps, _p(out), _dt(out), _s()), "kw_layernorm")
+    return out
+
+
+class GemmPlan:
+    """A pre-built ``kw_gemm`` / ``kw_gemv`` call: C = epilogue(A . W^T + bias)."""
+
+    def __init__(self, A, W, C, M, N, K, *, bias=None, lda=None, a_rows_per_batch=0, a_batch_stride=0,
+                 ldc=None, c_rows_per_batch=0, c_batch_stride=0, epilogue=L.KW_EPI_STORE, gelu=False,
+                 scale=1.0, scale_cols=0, row_add=None, row_add_period=0, hs_seq=0, hs_heads=0, hs_head_dim=0,
+                 packed=False, dtype=None, a_offset=0, c_offset=0):
+        _cuda(A, W, C, bias, row_add)
+        self._keep = (A, W, C, bias, row_add)
+        dt = _dt(W) if dtype is None else _DT[dtype]
+        a = L.GemmArgs()
+        a.dtype = dt
+        a.c_dtype = _dt(C)
+        a.A = A.data_ptr() + a_offset * A.element_size()
+        a.lda = K if lda is None else lda
+        a.a_rows_per_batch = a_rows_per_batch
+        a.a_batch_stride = a_batch_stride
+        a.W = W.data_ptr()
+        a.bias = bias.data_ptr() if bias is not None else None
+        a.C = C.data_ptr() + c_offset * C.element_size()
+        a.ldc = N if ldc is None else ldc
+        a.c_rows_per_batch = c_rows_per_batch
+        a.c_batch_stride = c_batch_stride
+        a.M, a.N, a.K = M, N, K
+        a.epilogue = epilogue
+        a.gelu = int(bool(gelu))
+        a.scale = float(scale)
+        a.scale_cols = scale_cols
+        a.row_add = row_add.data_ptr() if row_add is not None else None
+        a.row_add_period = row_add_period
+        a.hs_seq, a.hs_heads, a.hs_head_dim = hs_seq, hs_heads, hs_head_dim
+        if bias is not None and bias.dtype != torch.float32:
+            raise ValueError("bias must be float32")
+        if row_add is not None and row_add.dtype != torch.float32:
+            raise ValueError("row_add must be float32")
+        self.args = a
+        self.packed = packed
+        self._fn = _lib().kw_gemv if packed else _lib().kw_gemm
+        self._name = "kw_gemv" if packed else "kw_gemm"
+        self._ref = ctypes.byref(a)
+
+    def __call__(self):
+        L.check(self._fn(self._ref, _s()), self._name)
+
+
+def pack_weight(W: torch.Tensor) -> torch.Tensor:
+    """[N][K] bf16 -> packed 16x32-fragment layout for kw_gemv."""
+    _cuda(W)
+    if W.dtype != torch.bfloat16 or W.dim() != 2 or not W.is_contiguous():
+        raise ValueError("pack_weight expects a contiguous 2-D bfloat16 tensor")
+    n, k = W.shape
+    nbytes = _lib().kw_packed_weight_bytes(n, k)
+    out = torch.empty((nbytes // 2,), device=W.device, dtype=torch.bfloat16)
+    L.check(_lib().kw_pack_weight(_p(W), n, k, _p(out), _s()), "kw_pack_weight")
+    return out
+
+
+def attention(qkv: torch.Tensor, B: int, H: int, T: int, hd: int, out: torch.Tensor):
+    _cuda(qkv, out)
+    if qkv.numel() != 3 * B * H * T * hd or out.numel() != B * T * H * hd or qkv.dtype != out.dtype:
+        raise ValueError("attention: qkv must hold [3][B][H][T][hd] and out [B][T][H*hd] of one dtype")
+    L.check(_lib().kw_attention(_dt(qkv), _p(qkv), B, H, T, hd, _p(out), _s()), "kw_attention")
+    return out
+
+
+def embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h):
+    _cuda(ids, cur_len, tok_emb, pos_emb, h)
+    L.check(_lib().kw_embed(_dt(tok_emb), _p(ids), ids.stride(0), B, q_len, _p(cur_len), _p(tok_emb), _p(pos_emb),
+                            tok_emb.shape[1], _p(h), _s()), "kw_embed")
+
+
+def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out):
+    _cuda(qkv, k_cache, v_cache, cur_len, out)
+    L.check(_lib().kw_self_attn_step(_dt(qkv), _p(qkv), B, q_len, H, hd, _p(k_cache), _p(v_cache), t_max,
+                                     _p(cur_len), _p(out), _s()), "kw_self_attn_step")
+
+
+def cross_attn_workspace_bytes(B, q_len, H, hd, S) -> int:
+    return int(_lib().kw_cross_attn_workspace(B, q_len, H, hd, S))
+
+
+def cross_attn_step(q, B, q_len, H, hd, k, v, S, out, workspace):
+    _cuda(q, k, v, out, workspace)
+    L.check(_lib().kw_cross_attn_step(_dt(q), _p(q), B, q_len, H, hd, _p(k), _p(v), S, _p(out), _p(workspace),
+                                      workspace.numel() * workspace.element_size(), _s()), "kw_cross_attn_step")
+
+
+class SamplerPlan:
+    """Pre-built ``kw_greedy_step`` call (processors + argmax + stopping on device)."""
+
+    def __init__(self, logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, *,
+                 return_timestamps, ts_begin, no_ts_id, eos_id, pad_id, max_initial_ts, max_length, begin_index,
+                 scores_out=None):
+        _cuda(logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, scores_out)
+        self._keep = (logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, scores_out)
+        a = L.SamplerArgs()
+        a.logits = logits.data_ptr()
+        a.B, a.V = logits.shape
+        a.suppress_mask = suppress_mask.data_ptr()
+        a.begin_suppress = begin_suppress.data_ptr() if begin_suppress is not None else None
+        a.n_begin_suppress = begin_suppress.numel() if begin_suppress is not None else 0
+        a.return_timestamps = int(bool(return_timestamps))
+        a.ts_begin, a.no_ts_id, a.eos_id, a.pad_id = ts_begin, no_ts_id, eos_id, pad_id
+        a.max_initial_ts = -1 if max_initial_ts is None else max_initial_ts
+        a.ids = ids.data_ptr()
+        a.ids_stride = ids.stride(0)
+        a.cur_len = cur_len.data_ptr()
+        a.max_length = max_length
+        a.begin_index = begin_index
+        a.unfinished = unfinished.data_ptr()
+        a.counter = counter.data_ptr()
+        a.n_unfinished = n_unfinished.data_ptr()
+        a.scores_out = scores_out.data_ptr() if scores_out is not None else None
+        self.args = a
+        self._ref = ctypes.byref(a)
+
+    def __call__(self):
+        L.check(_lib().kw_greedy_step(self._ref, _s()), "kw_greedy_step")

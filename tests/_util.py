@@ -1,0 +1,44 @@
+"""Shared test helpers (inputs regenerated from seeds; expected values from tests/golden)."""
+from __future__ import annotations
+
+import json
+
+import numpy as np
+
+from kwhisper import synthetic as S
+from kwhisper.config import PRESETS, generation_constants
+
+
+def audio_cases(cases):
+    out = []
+    for c in cases:
+        kind, seed = str(c).split(":")
+        out.append(getattr(S, f"{kind}_audio")(int(seed)))
+    return np.stack(out)
+
+
+def gen_dict(shape, pad=None) -> dict:
+    return generation_constants(shape, pad_token_id=pad).to_dict()
+
+
+def oracle_features(shape, cases):
+    from oracle.mel import log_mel
+
+    return log_mel(audio_cases(cases), shape.num_mel_bins)
+
+
+def segments_of(fixture_value):
+    return json.loads(str(fixture_value))
+
+
+# mode name -> (generate kwargs, pad override) ; mirrors tools/make_fixtures.py
+BASE = dict(language="ja", task="transcribe")
+TINY_MODES = {
+    "greedy": (dict(BASE, return_timestamps=False), None),
+    "greedy_ts": (dict(BASE, return_timestamps=True), None),
+    "greedy_dict": (dict(BASE, return_timestamps=False, return_dict_in_generate=True), None),
+    "greedy_pad_eq_eos": (dict(BASE, return_timestamps=True), 50257),
+    "greedy_translate": (dict(language="ja", task="translate", return_timestamps=False), None),
+    "greedy_detect": (dict(return_timestamps=False), None),
+    "greedy_short": (dict(BASE, return_timestamps=False, max_length=16), None),
+}

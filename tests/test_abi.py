@@ -1,0 +1,74 @@
+"""CPU-side checks of the C-ABI library: it loads, exports every symbol the header declares, and the
+ctypes mirrors of the argument structs have the C layout (no GPU needed, no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+HEADER = os.path.join(ROOT, "include", "kwhisper.h")
+LIB = os.path.join(ROOT, "kotoba-whisper_amd", "kwhisper", "libkwhisper.so")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(kw_[a-z0-9_]+)\s*\(", src)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(LIB):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "kotoba-whisper_amd", "csrc"), "-j8"], check=True)
+    from kwhisper import _lib
+
+    return _lib.load()
+
+
+def test_exports_every_declared_symbol(lib):
+    names = _declared()
+    assert len(names) >= 15
+    for n in names:
+        assert hasattr(lib, n), n
+    from kwhisper import _lib
+
+    assert set(names) == set(_lib.EXPORTS), "ctypes binding and header disagree"
+
+
+def test_version(lib):
+    assert lib.kw_version() == 100
+
+
+def _c_layout(struct, fields):
+    code = "#include <stdio.h>\n#include <stddef.h>\n#include \"kwhisper.h\"\nint main(){"
+    code += f'printf("%zu\\n", sizeof({struct}));'
+    for f in fields:
+        code += f'printf("%zu\\n", offsetof({struct}, {f}));'
+    code += "return 0;}"
+    d = os.environ.get("TMPDIR", "/tmp")
+    src, exe = os.path.join(d, "kw_layout.c"), os.path.join(d, "kw_layout")
+    open(src, "w").write(code)
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), src, "-o", exe], check=True)
+    return [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
+
+
+@pytest.mark.parametrize("cname,pyname", [("kw_gemm_args", "GemmArgs"), ("kw_sampler_args", "SamplerArgs")])
+def test_struct_layout_matches_c(cname, pyname):
+    from kwhisper import _lib
+
+    cls = getattr(_lib, pyname)
+    fields = [f for f, _ in cls._fields_]
+    got = _c_layout(cname, fields)
+    assert got[0] == ctypes.sizeof(cls)
+    for f, off in zip(fields, got[1:]):
+        assert getattr(cls, f).offset == off, f
+
+
+def test_errors_are_returned_not_thrown(lib):
+    """Invalid arguments come back as KW_EINVAL with a message (no HIP call is made)."""
+    rc = lib.kw_layernorm(None, 1, 7, None, None, 1e-5, None, 0, None)
+    assert rc == 1
+    assert b"kw_layernorm" in lib.kw_last_error()

@@ -1,0 +1,138 @@
+"""End-to-end parity of the MI355X generate() against golden vectors from the reference path.
+
+fp32 engine: greedy token matrices must be bit-exact with transformers 5.15.0 (CPU, fp32) for every
+prompt / timestamp / padding mode of tests/golden/tiny_fp32.npz and for large-v3 / kotoba-v2.0.
+bf16 engine (the performance path): per-step teacher-forced logits within a stated tolerance of the
+fp32 reference, and greedy tokens equal wherever the reference's top-1/top-2 margin exceeds the
+bf16 noise floor.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from kwhisper.config import KOTOBA_V2, LARGE_V3, TINY, generation_constants  # noqa: E402
+from kwhisper.synthetic import synthetic_state_dict  # noqa: E402
+
+from _util import TINY_MODES, oracle_features  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _model(shape, dtype, pad=None):
+    from kwhisper.generation import KWhisperForConditionalGeneration
+
+    return KWhisperForConditionalGeneration.from_state_dict(
+        shape, synthetic_state_dict(shape, 0), dtype=dtype, generation_config=generation_constants(shape, pad))
+
+
+@pytest.fixture(scope="module")
+def tiny32():
+    return _model(TINY, torch.float32)
+
+
+@pytest.fixture(scope="module")
+def tiny16():
+    return _model(TINY, torch.bfloat16)
+
+
+def test_tiny_fp32_encoder(gold, tiny32):
+    g = gold("tiny_fp32")
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    enc = tiny32.get_encoder()(feats).last_hidden_state.cpu().numpy()
+    np.testing.assert_allclose(enc[:, ::50, :], g["enc_slice"], atol=2e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("mode", sorted(TINY_MODES))
+def test_tiny_fp32_generate_bitexact(gold, tiny32, mode):
+    g = gold("tiny_fp32")
+    kw, pad = TINY_MODES[mode]
+    kw = dict(kw)
+    model = tiny32
+    if pad is not None:
+        model.generation_config = generation_constants(TINY, pad)
+    try:
+        feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+        kw.setdefault("max_length", int(g["max_length"]))
+        res = model.generate(feats, **kw)
+        toks = res["sequences"] if isinstance(res, dict) else res
+        np.testing.assert_array_equal(toks.cpu().numpy(), g[f"{mode}_tokens"])
+    finally:
+        model.generation_config = generation_constants(TINY)
+
+
+def test_tiny_fp32_logits(gold, tiny32):
+    g = gold("tiny_fp32")
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    eng = tiny32.engine
+    sess = eng.new_session(feats.shape[0], eng.encode(feats))
+    seq = torch.from_numpy(g["greedy_sequences"])
+    lg = sess.teacher_forced_logits(seq[:, :-1], 4).cpu()
+    idx, val = g["greedy_logits_top_idx"], g["greedy_logits_top_val"]
+    got = torch.gather(lg[:, : idx.shape[1]], -1, torch.from_numpy(idx.astype(np.int64))).numpy()
+    np.testing.assert_allclose(got, val, atol=1e-3, rtol=0)  # north-star: logits within 1e-3 fp32
+
+
+def test_tiny_bf16_logits_and_tokens(gold, tiny16):
+    g = gold("tiny_fp32")
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    eng = tiny16.engine
+    sess = eng.new_session(feats.shape[0], eng.encode(feats))
+    seq = torch.from_numpy(g["greedy_sequences"])
+    lg = sess.teacher_forced_logits(seq[:, :-1], 4).cpu()
+    idx, val = g["greedy_logits_top_idx"], g["greedy_logits_top_val"]
+    got = torch.gather(lg[:, : idx.shape[1]], -1, torch.from_numpy(idx.astype(np.int64))).numpy()
+    err = np.abs(got - val)
+    print("tiny bf16 teacher-forced logit err: max %.4f mean %.4f" % (err.max(), err.mean()))
+    assert err.max() < 0.25 and err.mean() < 0.03   # bf16 weights/activations, f32 accumulation
+    toks = tiny16.generate(feats, language="ja", task="transcribe", max_length=128).cpu().numpy()
+    want = g["greedy_tokens"]
+    margin = g["greedy_margin"]
+    for b in range(want.shape[0]):
+        # tokens must agree up to the first step whose reference margin is within bf16 noise
+        unsafe = np.nonzero(margin[b] < 0.1)[0]
+        upto = unsafe[0] if unsafe.size else want.shape[1]
+        np.testing.assert_array_equal(toks[b, :upto], want[b, :upto])
+
+
+@pytest.mark.parametrize("shape,tag", [(LARGE_V3, "large_v3_fp32"), (KOTOBA_V2, "kotoba_v2_fp32")])
+def test_large_fp32_bitexact(gold, shape, tag):
+    g = gold(tag)
+    model = _model(shape, torch.float32)
+    feats = torch.from_numpy(oracle_features(shape, g["cases"])).cuda()
+    enc = model.get_encoder()(feats).last_hidden_state.cpu().numpy()
+    np.testing.assert_allclose(enc[:, ::50, :], g["enc_slice"], atol=5e-4, rtol=1e-3)
+    toks = model.generate(feats, language="ja", task="transcribe", max_length=int(g["max_length"]))
+    np.testing.assert_array_equal(toks.cpu().numpy(), g["greedy_tokens"])
+    if "greedy_ts_tokens" in g:
+        toks = model.generate(feats, language="ja", task="transcribe", return_timestamps=True, max_length=24)
+        np.testing.assert_array_equal(toks.cpu().numpy(), g["greedy_ts_tokens"])
+    del model
+    torch.cuda.empty_cache()
+
+
+def test_large_bf16_vs_reference(gold):
+    g = gold("large_v3_fp32")
+    model = _model(LARGE_V3, torch.bfloat16)
+    feats = torch.from_numpy(oracle_features(LARGE_V3, g["cases"])).cuda()
+    eng = model.engine
+    enc = eng.encode(feats)
+    e = enc.view(2, 1500, 1280).float().cpu().numpy()[:, ::50, :]
+    rel = np.abs(e - g["enc_slice"]).max() / np.abs(g["enc_slice"]).max()
+    print("large-v3 bf16 encoder rel err", rel)
+    assert rel < 0.05
+    sess = eng.new_session(2, enc)
+    seq = torch.from_numpy(g["greedy_sequences"])
+    lg = sess.teacher_forced_logits(seq[:, :-1], 4).cpu()
+    idx, val = g["greedy_logits_top_idx"], g["greedy_logits_top_val"]
+    got = torch.gather(lg[:, : idx.shape[1]], -1, torch.from_numpy(idx.astype(np.int64))).numpy()
+    err = np.abs(got - val)
+    print("large-v3 bf16 teacher-forced logit err: max %.4f mean %.4f" % (err.max(), err.mean()))
+    assert err.mean() < 0.1
+    del model, sess
+    torch.cuda.empty_cache()

@@ -1,0 +1,315 @@
+"""Kernel-level parity on the MI355X: every C-ABI entry point against the oracle / an fp32 reference.
+
+Floating-point tolerances are stated per test.  Integer / index outputs (tokens, argmax, ids) are
+compared exactly.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from kwhisper import _lib as L  # noqa: E402
+from kwhisper import ops  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L.load()
+    torch.manual_seed(0)
+
+
+def dev(x, dtype=None):
+    t = torch.as_tensor(x)
+    return t.to("cuda", dtype or t.dtype).contiguous()
+
+
+# ---------------------------------------------------------------- log-mel (a1)
+@pytest.mark.parametrize("n_mels", [80, 128])
+def test_log_mel_vs_oracle(n_mels):
+    from oracle.mel import log_mel, mel_filters, pad_or_trim
+    from kwhisper import synthetic as S
+    from kwhisper.feature_extraction import mel_filter_bank
+
+    clips = [S.dummy_audio(0), S.dummy_audio(1), S.tone_audio(0), S.tone_audio(1),
+             pad_or_trim(S.tone_audio(2)[:24000]), np.zeros(480000, np.float32)]
+    audio = np.stack(clips)
+    fb = mel_filter_bank(201, n_mels, 0.0, 8000.0, 16000)
+    np.testing.assert_allclose(fb, mel_filters(n_mels), rtol=1e-12, atol=1e-15)  # product bank == oracle bank
+    got = ops.log_mel(dev(audio), dev(fb.astype(np.float32))).cpu().numpy()
+    want = log_mel(audio, n_mels)
+    err = np.abs(got - want).max()
+    print("log-mel max abs err", err)
+    # reference's own numpy-vs-torch tolerance is 1e-5 (feature_extraction_whisper.py:107)
+    assert err < 2e-5
+
+
+def test_log_mel_rejects_bad_length():
+    with pytest.raises(ValueError):
+        ops.log_mel(torch.zeros((1, 1000), device="cuda"), torch.zeros((201, 80), device="cuda"))
+
+
+# ---------------------------------------------------------------- GEMMs
+def _ref_gemm(A, W, bias):
+    return A.float() @ W.float().t() + (bias if bias is not None else 0)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 128, 64), (6000, 1152, 384), (1000, 384, 1536), (48000, 1280, 1280)])
+def test_gemm_bf16_store(M, N, K):
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda")
+    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.GemmPlan(A, W, C, M, N, K, bias=b)()
+    ref = _ref_gemm(A, W, b)
+    torch.testing.assert_close(C.float(), ref, atol=2e-2, rtol=1e-2)
+
+
+def test_gemm_bf16_epilogues():
+    M, N, K = 300, 256, 128
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda")
+    ref = _ref_gemm(A, W, b)
+    # gelu + column scale + row_add (period 7) into f32
+    ra = torch.randn(7, N, device="cuda")
+    C = torch.empty(M, N, device="cuda")
+    ops.GemmPlan(A, W, C, M, N, K, bias=b, gelu=True, scale=0.125, scale_cols=100, row_add=ra, row_add_period=7)()
+    r = torch.nn.functional.gelu(ref)
+    r[:, :100] *= 0.125
+    r += ra[torch.arange(M, device="cuda") % 7]
+    torch.testing.assert_close(C, r, atol=1e-3, rtol=1e-3)
+    # residual add
+    H0 = torch.randn(M, N, device="cuda")
+    Hc = H0.clone()
+    ops.GemmPlan(A, W, Hc, M, N, K, bias=b, epilogue=L.KW_EPI_RESID)()
+    torch.testing.assert_close(Hc, H0 + ref, atol=1e-3, rtol=1e-3)
+
+
+def test_gemm_bf16_headsplit():
+    B, T, H, hd = 2, 100, 2, 64
+    d = H * hd
+    M, N, K = B * T, 3 * d, 128
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda")
+    C = torch.empty(3, B, H, T, hd, device="cuda", dtype=torch.bfloat16)
+    ops.GemmPlan(A, W, C, M, N, K, bias=b, epilogue=L.KW_EPI_HEADSPLIT, scale=0.125, scale_cols=d,
+                 hs_seq=T, hs_heads=H, hs_head_dim=hd)()
+    ref = _ref_gemm(A, W, b)
+    ref[:, :d] *= 0.125
+    ref = ref.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+    torch.testing.assert_close(C.float(), ref, atol=2e-2, rtol=1e-2)
+
+
+def test_gemm_conv_rowmap():
+    """Conv1d(k3, p1, stride 1 and 2) as GEMM over the time-major padded layout."""
+    B, C, T, d = 2, 80, 3000, 256
+    mel = torch.randn(B, C, T, device="cuda")
+    w1 = torch.randn(d, C, 3, device="cuda") / (3 * C) ** 0.5
+    b1 = torch.randn(d, device="cuda")
+    w2 = torch.randn(d, d, 3, device="cuda") / (3 * d) ** 0.5
+    b2 = torch.randn(d, device="cuda")
+    c_pad = 128
+    tm = ops.mel_to_time_major(mel, c_pad, torch.bfloat16)
+    w1p = torch.zeros(d, 3, c_pad, device="cuda")
+    w1p[:, :, :C] = w1.permute(0, 2, 1)
+    w1p = w1p.reshape(d, 3 * c_pad).bfloat16().contiguous()
+    conv = torch.zeros(B, T + 2, d, device="cuda", dtype=torch.bfloat16)
+    ops.GemmPlan(tm, w1p, conv, B * T, d, 3 * c_pad, bias=b1, lda=c_pad, a_rows_per_batch=T,
+                 a_batch_stride=(T + 2) * c_pad, ldc=d, c_rows_per_batch=T, c_batch_stride=(T + 2) * d, c_offset=d,
+                 gelu=True)()
+    ref1 = torch.nn.functional.gelu(torch.nn.functional.conv1d(mel.bfloat16().float(), w1.bfloat16().float(), b1, padding=1))
+    torch.testing.assert_close(conv[:, 1:-1].float().permute(0, 2, 1), ref1, atol=3e-2, rtol=2e-2)
+    assert conv[:, 0].abs().max() == 0 and conv[:, -1].abs().max() == 0
+    w2p = w2.permute(0, 2, 1).reshape(d, 3 * d).bfloat16().contiguous()
+    Tn = T // 2
+    pos = torch.randn(Tn, d, device="cuda")
+    h = torch.empty(B * Tn, d, device="cuda")
+    ops.GemmPlan(conv, w2p, h, B * Tn, d, 3 * d, bias=b2, lda=2 * d, a_rows_per_batch=Tn,
+                 a_batch_stride=(T + 2) * d, gelu=True, row_add=pos, row_add_period=Tn)()
+    ref2 = torch.nn.functional.gelu(torch.nn.functional.conv1d(conv[:, 1:-1].float().permute(0, 2, 1),
+                                                                w2.bfloat16().float(), b2, stride=2, padding=1))
+    ref2 = ref2.permute(0, 2, 1) + pos
+    torch.testing.assert_close(h.view(B, Tn, d), ref2, atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(37, 100, 48), (512, 1280, 1280), (4, 51865, 384)])
+def test_gemm_f32_exactish(M, N, K):
+    A = torch.randn(M, K, device="cuda")
+    W = torch.randn(N, K, device="cuda") / K ** 0.5
+    b = torch.randn(N, device="cuda")
+    C = torch.empty(M, N, device="cuda")
+    ops.GemmPlan(A, W, C, M, N, K, bias=b)()
+    ref = (A.double() @ W.double().t() + b.double()).float()
+    torch.testing.assert_close(C, ref, atol=2e-5, rtol=2e-5)
+
+
+@pytest.mark.parametrize("M,N,K", [(1, 1280, 1280), (32, 3840, 1280), (32, 1280, 5120), (128, 5120, 1280),
+                                   (5, 51866, 1280), (32, 51865, 384)])
+def test_gemv_packed(M, N, K):
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda")
+    Wp = ops.pack_weight(W)
+    C = torch.empty(M, N, device="cuda")
+    ops.GemmPlan(A, Wp, C, M, N, K, bias=b, packed=True, dtype=torch.bfloat16)()
+    torch.testing.assert_close(C, _ref_gemm(A, W, b), atol=2e-3, rtol=2e-3)
+    H0 = torch.randn(M, N, device="cuda")
+    Hc = H0.clone()
+    ops.GemmPlan(A, Wp, Hc, M, N, K, bias=b, packed=True, epilogue=L.KW_EPI_RESID, dtype=torch.bfloat16)()
+    torch.testing.assert_close(Hc, H0 + _ref_gemm(A, W, b), atol=2e-3, rtol=2e-3)
+
+
+# ---------------------------------------------------------------- LayerNorm
+@pytest.mark.parametrize("rows,dim", [(1, 384), (48000, 1280), (33, 2048)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_layernorm(rows, dim, out_dtype):
+    x = torch.randn(rows, dim, device="cuda") * 3 + 1
+    g = torch.randn(dim, device="cuda")
+    b = torch.randn(dim, device="cuda")
+    y = torch.empty(rows, dim, device="cuda", dtype=out_dtype)
+    ops.layernorm(x, g, b, 1e-5, y)
+    ref = torch.nn.functional.layer_norm(x.double(), (dim,), g.double(), b.double(), 1e-5).float()
+    tol = 1e-5 if out_dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float(), ref, atol=tol * 4, rtol=tol)
+
+
+# ---------------------------------------------------------------- attention
+def _ref_attn(qkv, B, H, T, hd):
+    q, k, v = qkv.float().view(3, B, H, T, hd)
+    p = torch.softmax(q @ k.transpose(-1, -2), -1)
+    return (p @ v).permute(0, 2, 1, 3).reshape(B, T, H * hd)
+
+
+@pytest.mark.parametrize("B,H,T", [(1, 1, 64), (2, 3, 100), (2, 20, 1500), (1, 2, 1)])
+def test_attention_bf16(B, H, T):
+    hd = 64
+    qkv = (torch.randn(3, B, H, T, hd, device="cuda") * 0.5).bfloat16()
+    qkv[0] *= 0.125 * 8  # pre-scaled q of unit-ish size
+    out = torch.empty(B, T, H * hd, device="cuda", dtype=torch.bfloat16)
+    ops.attention(qkv, B, H, T, hd, out)
+    torch.testing.assert_close(out.float(), _ref_attn(qkv, B, H, T, hd), atol=2e-2, rtol=2e-2)
+
+
+def test_attention_bf16_spike():
+    """Force the online-softmax rescale: one key dominates one query late in the sequence."""
+    B, H, T, hd = 1, 1, 1500, 64
+    qkv = (torch.randn(3, B, H, T, hd, device="cuda") * 0.3)
+    qkv[1, 0, 0, 1400] = qkv[0, 0, 0, 5] * 40
+    qkv = qkv.bfloat16()
+    out = torch.empty(B, T, H * hd, device="cuda", dtype=torch.bfloat16)
+    ops.attention(qkv, B, H, T, hd, out)
+    torch.testing.assert_close(out.float(), _ref_attn(qkv, B, H, T, hd), atol=3e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("B,H,T", [(2, 3, 100), (1, 6, 1500)])
+def test_attention_f32(B, H, T):
+    hd = 64
+    qkv = torch.randn(3, B, H, T, hd, device="cuda") * 0.5
+    out = torch.empty(B, T, H * hd, device="cuda")
+    ops.attention(qkv, B, H, T, hd, out)
+    ref = _ref_attn(qkv.double(), B, H, T, hd).float()
+    torch.testing.assert_close(out, ref, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("q_len", [1, 4])
+def test_self_attn_step(dtype, q_len):
+    B, H, hd, t_max = 3, 4, 64, 448
+    d = H * hd
+    kc = torch.zeros(B, H, t_max, hd, device="cuda", dtype=dtype)
+    vc = torch.zeros_like(kc)
+    past = 10
+    kc[:, :, :past] = torch.randn(B, H, past, hd, device="cuda").to(dtype)
+    vc[:, :, :past] = torch.randn(B, H, past, hd, device="cuda").to(dtype)
+    qkv = torch.randn(B * q_len, 3 * d, device="cuda").to(dtype)
+    cur = torch.tensor([past + q_len], device="cuda", dtype=torch.int32)
+    out = torch.empty(B * q_len, d, device="cuda", dtype=dtype)
+    ops.self_attn_step(qkv, B, q_len, H, hd, kc, vc, t_max, cur, out)
+    x = qkv.float().view(B, q_len, 3, H, hd)
+    k_all = torch.cat([kc[:, :, :past].float(), x[:, :, 1].permute(0, 2, 1, 3)], 2)
+    v_all = torch.cat([vc[:, :, :past].float(), x[:, :, 2].permute(0, 2, 1, 3)], 2)
+    q = x[:, :, 0].permute(0, 2, 1, 3)
+    s = q @ k_all.transpose(-1, -2)
+    mask = torch.arange(past + q_len, device="cuda")[None, :] > (torch.arange(q_len, device="cuda")[:, None] + past)
+    s = s.masked_fill(mask, float("-inf"))
+    ref = (torch.softmax(s, -1) @ v_all).permute(0, 2, 1, 3).reshape(B * q_len, d)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
+    torch.testing.assert_close(kc[:, :, past:past + q_len].float(), x[:, :, 1].permute(0, 2, 1, 3))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("q_len,S", [(1, 1500), (3, 1500), (1, 77)])
+def test_cross_attn_step(dtype, q_len, S):
+    B, H, hd = 3, 4, 64
+    d = H * hd
+    k = torch.randn(B, H, S, hd, device="cuda").to(dtype)
+    v = torch.randn(B, H, S, hd, device="cuda").to(dtype)
+    q = (torch.randn(B * q_len, d, device="cuda") * 0.3).to(dtype)
+    out = torch.empty(B * q_len, d, device="cuda", dtype=dtype)
+    ws = torch.empty(ops.cross_attn_workspace_bytes(B, q_len, H, hd, S) // 4 + 1, device="cuda")
+    ops.cross_attn_step(q, B, q_len, H, hd, k, v, S, out, ws)
+    qq = q.float().view(B, q_len, H, hd).permute(0, 2, 1, 3)
+    ref = (torch.softmax(qq @ k.float().transpose(-1, -2), -1) @ v.float()).permute(0, 2, 1, 3).reshape(B * q_len, d)
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
+
+
+# ---------------------------------------------------------------- greedy step (processors + argmax)
+def _random_history(rng, B, P, n, ts_begin, V, eos, pad):
+    ids = np.zeros((B, P + n), np.int64)
+    ids[:, :P] = [50258, 50266, 50360][:P] if P <= 3 else 0
+    for b in range(B):
+        for j in range(n):
+            r = rng.random()
+            ids[b, P + j] = rng.integers(ts_begin, V) if r < 0.4 else rng.integers(0, eos)
+    ids[1, P + n - 2:] = [eos, pad] if n >= 2 else ids[1, P + n - 2:]
+    return ids
+
+
+@pytest.mark.parametrize("rt", [False, True])
+@pytest.mark.parametrize("n_hist", [0, 1, 2, 5, 30])
+def test_greedy_step_vs_oracle(rt, n_hist):
+    from kwhisper.config import LARGE_V3, generation_constants
+    from oracle.generate import process_logits
+
+    gen = generation_constants(LARGE_V3)
+    V = LARGE_V3.vocab_size
+    B, P = 6, 3
+    rng = np.random.default_rng(n_hist + 100 * rt)
+    hist = _random_history(rng, B, P, n_hist, gen.timestamp_begin, V, gen.eos_token_id, gen.pad_token_id)
+    logits = rng.standard_normal((B, V)).astype(np.float32) * 3
+    logits[:, gen.timestamp_begin:] += 2.0 * (np.arange(B)[:, None] % 2)  # some rows favour timestamps
+    gd = gen.to_dict()
+    want = process_logits(hist, logits, gd, P, rt)
+    L_now = hist.shape[1]
+    ids = torch.zeros((B, 449), dtype=torch.int64, device="cuda")
+    ids[:, :L_now] = torch.from_numpy(hist)
+    cur = torch.tensor([L_now], dtype=torch.int32, device="cuda")
+    unf = torch.ones(B, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    nun = torch.zeros(1, dtype=torch.int32, device="cuda")
+    sup = torch.zeros(V, dtype=torch.uint8)
+    sup[torch.tensor(gen.suppress_tokens)] = 1
+    scores = torch.empty((B, V), device="cuda")
+    lg = dev(logits)
+    plan = ops.SamplerPlan(lg, sup.cuda(), torch.tensor(gen.begin_suppress_tokens, dtype=torch.int32, device="cuda"),
+                           ids, cur, unf, cnt, nun, return_timestamps=rt, ts_begin=gen.timestamp_begin,
+                           no_ts_id=gen.no_timestamps_token_id, eos_id=gen.eos_token_id, pad_id=gen.pad_token_id,
+                           max_initial_ts=gen.max_initial_timestamp_index, max_length=448, begin_index=P,
+                           scores_out=scores)
+    plan()
+    torch.cuda.synchronize()
+    got = scores.cpu().numpy()
+    np.testing.assert_array_equal(np.isneginf(got), np.isneginf(want))
+    fin = [(hist[b, P:] == gen.eos_token_id).any() for b in range(B)]
+    tok = ids[:, L_now].cpu().numpy()
+    for b in range(B):
+        exp_tok = gen.pad_token_id if fin[b] else int(np.argmax(want[b]))
+        assert tok[b] == exp_tok
+    assert int(cur.item()) == L_now + 1
+    assert int(nun.item()) == int(unf.sum().item())
