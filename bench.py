@@ -131,7 +131,13 @@ def main():
     qx = sess._buffers(1)["qx"]
     attn_out = sess._buffers(1)["attn"]
     ws = sess._buffers(1)["ws"]
-    cross_t = time_fn(lambda: ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[0], sess.cross[1], S, attn_out, ws), iters)
+    n_dec = shape.decoder_layers
+
+    def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
+        for li in range(n_dec):
+            ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[2 * li], sess.cross[2 * li + 1], S, attn_out, ws)
+
+    cross_t = time_fn(cross_all_layers, max(1, iters // 4)) / n_dec
     cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
     feats = fe.extract(audio)
     enc_t = time_fn(lambda: eng.encode(feats), 3)

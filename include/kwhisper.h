@@ -29,7 +29,7 @@ enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
 enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 
 /* ABI version (major*100 + minor) and the last error message of this thread. */
-int kw_version(void);
+int kw_version(void);  /* 102 */
 const char* kw_last_error(void);
 
 /* a1 -- log-mel spectrogram.
@@ -73,15 +73,34 @@ typedef struct {
   const float* row_add;      /* [period][N] f32 added after the activation, or NULL */
   int64_t row_add_period;
   int64_t hs_seq, hs_heads, hs_head_dim;
+  /* kw_gemv only -- fused LayerNorm prologue: if ln_h != NULL, A = (ln_h - mean) * rstd is formed on
+   * the fly (ln_h [M][K] f32, row pitch lda) from row statistics ln_stats [M][ln_slots][2] holding
+   * partial (sum, sum of squares) per slot, and ln_eps (modeling_whisper.py:434-446).  The
+   * LayerNorm's gamma/beta are NOT applied: fold them into the weights when loading them,
+   * W' = W diag(gamma), bias' = bias + W beta. */
+  const float* ln_h;
+  const float* ln_stats;
+  int64_t ln_slots;
+  float ln_eps;
+  /* kw_gemv RESID only: per-row (sum, sum of squares) of the UPDATED C over each 16-column block,
+   * written to stats_out[M][ceil(N/16)][2] -- the statistics of the next LayerNorm.  NULL = skip. */
+  float* stats_out;
+  /* kw_gemv split-K scratch (partial tiles + arrival counters): >= kw_gemv_workspace_bytes(M, N, K)
+   * bytes, ZERO-FILLED before first use (every call leaves the counters zero).  May be shared by all
+   * kw_gemv calls issued in order on one stream. */
+  void* workspace;
+  size_t ws_bytes;
 } kw_gemm_args;
 
 int kw_gemm(const kw_gemm_args* args, kw_stream_t stream);
 
 /* Skinny GEMM for decode steps (M <= 128): same contract as kw_gemm (STORE / RESID epilogues,
- * no row maps), W pre-packed by kw_pack_weight (bf16 only). */
+ * no row maps), W pre-packed by kw_pack_weight (bf16 only); optional fused LayerNorm prologue and
+ * row-statistics epilogue (fields ln_* / stats_out above). */
 int kw_gemv(const kw_gemm_args* args, kw_stream_t stream);
 /* W [N][K] bf16 -> packed [ceil(N/16)][K/32][64 lanes][8] bf16 (rows >= N zero); K % 32 == 0. */
 int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed, kw_stream_t stream);
+size_t kw_gemv_workspace_bytes(int64_t M, int64_t N, int64_t K);
 size_t kw_packed_weight_bytes(int64_t N, int64_t K);
 
 /* LayerNorm (eps) over the last dim of x [rows][dim] f32 -> y [rows][dim] (y_dtype);
@@ -98,7 +117,8 @@ int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, int64_t T, in
  * with L = *cur_len read on device (TF modeling_whisper.py:737-762; no embed scale). */
 int kw_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
              const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
-             kw_stream_t stream);
+             float* stats_out, kw_stream_t stream);
+/* (stats_out: optional [B*q_len][1][2] row (sum, sum of squares) of h for a fused LayerNorm.) */
 
 /* Decoder self-attention over a static cache (TF modeling_whisper.py:469-480, cache_utils.py:127-145):
  * appends k/v of the q_len newest positions [L-q_len, L) to k_cache/v_cache [B][H][t_max][hd],
@@ -108,7 +128,8 @@ int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t q_len, int6
                       kw_stream_t stream);
 
 /* Decoder cross-attention against cached encoder K/V [B][H][S][hd] (TF modeling_whisper.py:323-326).
- * q: [B*q_len][H*hd]; out: [B*q_len][H*hd]; workspace >= kw_cross_attn_workspace(...) bytes. */
+ * q: [B*q_len][H*hd]; out: [B*q_len][H*hd]; workspace >= kw_cross_attn_workspace(...) bytes and
+ * ZERO-FILLED before its first use (it holds arrival counters that every call leaves at zero). */
 int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64_t H, int64_t hd,
                        const void* k, const void* v, int64_t S, void* out, void* workspace,
                        size_t ws_bytes, kw_stream_t stream);

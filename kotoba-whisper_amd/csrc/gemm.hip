@@ -13,56 +13,10 @@
 //    come from L2; 4 waves split K and reduce through LDS.  HBM-bound (weights read once per step).
 // Shared epilogues: bias, exact GELU, column scale (q * head_dim^-0.5, modeling_whisper.py:309),
 // row-periodic add (encoder positions, :621-624), residual add into the f32 stream, head-split store.
-#include "kw_common.h"
+#include "gemm_common.h"
 
 namespace {
-
-struct GemmP {
-  const void* A;
-  int64_t lda, a_rpb, a_bs;
-  const void* W;
-  const float* bias;
-  void* C;
-  int64_t ldc, c_rpb, c_bs;
-  int M, N, K;
-  int gelu;
-  float scale;
-  int scale_cols;
-  const float* row_add;
-  int row_add_period;
-  int hs_seq, hs_heads, hs_hd;
-};
-
-__device__ __forceinline__ int64_t row_off(int64_t r, int64_t rpb, int64_t bs, int64_t ld) {
-  const int64_t b = r / rpb;
-  return b * bs + (r - b * rpb) * ld;
-}
-
-template <int EPI, typename TC>
-__device__ __forceinline__ void epi_one(const GemmP& p, int m, int n, float v, float bias_n) {
-  v += bias_n;
-  if constexpr (EPI == KW_EPI_RESID) {
-    float* c = reinterpret_cast<float*>(p.C) + row_off(m, p.c_rpb, p.c_bs, p.ldc) + n;
-    *c += v;
-  } else {
-    if (p.gelu) v = gelu_erf(v);
-    if (n < p.scale_cols) v *= p.scale;
-    if (p.row_add) v += p.row_add[(int64_t)(m % p.row_add_period) * p.N + n];
-    int64_t off;
-    if constexpr (EPI == KW_EPI_HEADSPLIT) {
-      const int width = p.hs_heads * p.hs_hd;
-      const int part = n / width;
-      const int rem = n - part * width;
-      const int h = rem / p.hs_hd, d = rem - h * p.hs_hd;
-      const int b = m / p.hs_seq, t = m - b * p.hs_seq;
-      const int nb = p.M / p.hs_seq;
-      off = ((((int64_t)part * nb + b) * p.hs_heads + h) * p.hs_seq + t) * p.hs_hd + d;
-    } else {
-      off = row_off(m, p.c_rpb, p.c_bs, p.ldc) + n;
-    }
-    TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + off, v);
-  }
-}
+using namespace kwg;
 
 // ------------------------------------------------------------------------------------------------
 // bf16 128x128x64, glds staging
@@ -215,104 +169,6 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmP p) {
   }
 }
 
-// ------------------------------------------------------------------------------------------------
-// decode skinny GEMM over packed weights
-// ------------------------------------------------------------------------------------------------
-constexpr int GV_WAVES = 4;
-constexpr int GV_MAXRB = 8;  // 8 x 16 = 128 rows
-
-template <int EPI, typename TC>
-__global__ __launch_bounds__(GV_WAVES * 64) void gemv_packed_kernel(GemmP p) {
-  __shared__ float red[GV_WAVES][GV_MAXRB][64][4];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int cb = blockIdx.x;
-  const int nkt = p.K >> 5;
-  const int nrb = (p.M + 15) >> 4;
-  const bf16x8* Wp = reinterpret_cast<const bf16x8*>(p.W) + (int64_t)cb * nkt * 64 + lane;
-  const bf16_t* A = reinterpret_cast<const bf16_t*>(p.A);
-  const int kt0 = (nkt * wave) / GV_WAVES, kt1 = (nkt * (wave + 1)) / GV_WAVES;
-  f32x4 acc[GV_MAXRB];
-#pragma unroll
-  for (int rb = 0; rb < GV_MAXRB; ++rb) acc[rb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int arow = lane & 15, akoff = 8 * (lane >> 4);
-  bf16x8 zero;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) zero[j] = (__bf16)0.f;
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const bf16x8 bfrag = __builtin_nontemporal_load(Wp + (int64_t)kt * 64);
-#pragma unroll
-    for (int rb = 0; rb < GV_MAXRB; ++rb) {
-      if (rb < nrb) {
-        const int m = rb * 16 + arow;
-        const bf16x8 afrag = m < p.M ? *reinterpret_cast<const bf16x8*>(A + (int64_t)m * p.lda + kt * 32 + akoff) : zero;
-        acc[rb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, bfrag, acc[rb], 0, 0, 0);
-      }
-    }
-  }
-#pragma unroll
-  for (int rb = 0; rb < GV_MAXRB; ++rb)
-    if (rb < nrb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) red[wave][rb][lane][r] = acc[rb][r];
-  __syncthreads();
-  // 16 columns x (nrb*16) rows; C/D: col = lane&15, row = (lane>>4)*4 + r
-  for (int o = tid; o < nrb * 256; o += GV_WAVES * 64) {
-    const int rb = o >> 8, rem = o & 255, l = rem >> 2, r = rem & 3;
-    float v = 0.f;
-#pragma unroll
-    for (int w = 0; w < GV_WAVES; ++w) v += red[w][rb][l][r];
-    const int m = rb * 16 + (l >> 4) * 4 + r;
-    const int n = cb * 16 + (l & 15);
-    if (m < p.M && n < p.N) epi_one<EPI, TC>(p, m, n, v, p.bias ? p.bias[n] : 0.f);
-  }
-}
-
-__global__ void pack_kernel(const bf16_t* __restrict__ W, int N, int K, bf16_t* __restrict__ out) {
-  const int nkt = K >> 5;
-  const int64_t total = (int64_t)((N + 15) >> 4) * nkt * 64;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
-    const int lane = (int)(i & 63);
-    const int64_t tile = i >> 6;
-    const int kt = (int)(tile % nkt);
-    const int cb = (int)(tile / nkt);
-    const int n = cb * 16 + (lane & 15);
-    const int k = kt * 32 + 8 * (lane >> 4);
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (n < N) v = *reinterpret_cast<const uint4*>(W + (int64_t)n * K + k);
-    reinterpret_cast<uint4*>(out)[i] = v;
-  }
-}
-
-GemmP to_params(const kw_gemm_args* a) {
-  GemmP p;
-  p.A = a->A; p.lda = a->lda;
-  p.a_rpb = a->a_rows_per_batch > 0 ? a->a_rows_per_batch : a->M;
-  p.a_bs = a->a_batch_stride;
-  p.W = a->W; p.bias = a->bias; p.C = a->C; p.ldc = a->ldc;
-  p.c_rpb = a->c_rows_per_batch > 0 ? a->c_rows_per_batch : a->M;
-  p.c_bs = a->c_batch_stride;
-  p.M = (int)a->M; p.N = (int)a->N; p.K = (int)a->K;
-  p.gelu = a->gelu; p.scale = a->scale; p.scale_cols = (int)a->scale_cols;
-  p.row_add = a->row_add; p.row_add_period = a->row_add_period > 0 ? (int)a->row_add_period : 1;
-  p.hs_seq = a->hs_seq > 0 ? (int)a->hs_seq : 1; p.hs_heads = a->hs_heads > 0 ? (int)a->hs_heads : 1;
-  p.hs_hd = a->hs_head_dim > 0 ? (int)a->hs_head_dim : 1;
-  if (p.c_rpb <= 0) p.c_rpb = 1;
-  if (p.a_rpb <= 0) p.a_rpb = 1;
-  return p;
-}
-
-int check_common(const kw_gemm_args* a) {
-  if (!a || !a->A || !a->W || !a->C || a->M < 0 || a->N <= 0 || a->K <= 0)
-    return kw_set_error_msg(KW_EINVAL, "kw_gemm: null pointer or bad sizes");
-  if (a->epilogue == KW_EPI_RESID && a->c_dtype != KW_DT_F32)
-    return kw_set_error_msg(KW_EINVAL, "kw_gemm: RESID epilogue needs an f32 C");
-  if (a->epilogue == KW_EPI_HEADSPLIT && (a->hs_seq <= 0 || a->hs_heads <= 0 || a->hs_head_dim <= 0 ||
-                                          a->M % a->hs_seq != 0 || a->N % (a->hs_heads * a->hs_head_dim) != 0))
-    return kw_set_error_msg(KW_EINVAL, "kw_gemm: bad head-split geometry");
-  if (a->epilogue < 0 || a->epilogue > 2) return kw_set_error_msg(KW_EINVAL, "kw_gemm: bad epilogue");
-  return KW_OK;
-}
-
 template <typename TC>
 hipError_t launch_bf16(const GemmP& p, int epi, hipStream_t s) {
   const int nwg = ((p.M + BM - 1) / BM) * (p.N / BN);
@@ -338,17 +194,6 @@ hipError_t launch_f32(const GemmP& p, int epi, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <typename TC>
-hipError_t launch_gemv(const GemmP& p, int epi, hipStream_t s) {
-  dim3 grid((p.N + 15) / 16);
-  switch (epi) {
-    case KW_EPI_STORE: hipLaunchKernelGGL((gemv_packed_kernel<KW_EPI_STORE, TC>), grid, dim3(GV_WAVES * 64), 0, s, p); break;
-    case KW_EPI_RESID: hipLaunchKernelGGL((gemv_packed_kernel<KW_EPI_RESID, float>), grid, dim3(GV_WAVES * 64), 0, s, p); break;
-    default: hipLaunchKernelGGL((gemv_packed_kernel<KW_EPI_HEADSPLIT, TC>), grid, dim3(GV_WAVES * 64), 0, s, p); break;
-  }
-  return hipGetLastError();
-}
-
 }  // namespace
 
 extern "C" int kw_gemm(const kw_gemm_args* a, kw_stream_t stream) {
@@ -370,32 +215,5 @@ extern "C" int kw_gemm(const kw_gemm_args* a, kw_stream_t stream) {
     return kw_set_error_msg(KW_EUNSUPPORTED, "kw_gemm: unsupported dtype");
   }
   if (e != hipSuccess) return kw_set_error(e);
-  return KW_OK;
-}
-
-extern "C" int kw_gemv(const kw_gemm_args* a, kw_stream_t stream) {
-  int rc = check_common(a);
-  if (rc) return rc;
-  if (a->dtype != KW_DT_BF16) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_gemv: bf16 only (use kw_gemm for f32)");
-  if (a->M > 16 * GV_MAXRB || a->K % 32 != 0 || a->lda % 8 != 0 || a->epilogue == KW_EPI_HEADSPLIT)
-    return kw_set_error_msg(KW_EINVAL, "kw_gemv: needs M <= 128, K % 32 == 0, lda % 8 == 0, no head-split");
-  if (a->M == 0) return KW_OK;
-  GemmP p = to_params(a);
-  p.a_rpb = p.M > 0 ? p.M : 1;
-  p.c_rpb = p.M > 0 ? p.M : 1;
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e = a->c_dtype == KW_DT_F32 ? launch_gemv<float>(p, a->epilogue, s) : launch_gemv<bf16_t>(p, a->epilogue, s);
-  if (e != hipSuccess) return kw_set_error(e);
-  return KW_OK;
-}
-
-extern "C" size_t kw_packed_weight_bytes(int64_t N, int64_t K) { return (size_t)((N + 15) / 16) * (size_t)K * 16 * 2; }
-
-extern "C" int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed, kw_stream_t stream) {
-  if (!W || !packed || N <= 0 || K <= 0 || K % 32 != 0)
-    return kw_set_error_msg(KW_EINVAL, "kw_pack_weight: needs K % 32 == 0");
-  hipLaunchKernelGGL(pack_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)W, (int)N, (int)K,
-                     (bf16_t*)packed);
-  KW_CHECK_LAUNCH();
   return KW_OK;
 }

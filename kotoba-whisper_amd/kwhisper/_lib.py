@@ -35,6 +35,9 @@ class GemmArgs(ctypes.Structure):
         ("scale", ctypes.c_float), ("scale_cols", c_i64),
         ("row_add", c_vp), ("row_add_period", c_i64),
         ("hs_seq", c_i64), ("hs_heads", c_i64), ("hs_head_dim", c_i64),
+        ("ln_h", c_vp), ("ln_stats", c_vp), ("ln_slots", c_i64),
+        ("ln_eps", ctypes.c_float), ("stats_out", c_vp),
+        ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
     ]
 
 
@@ -60,9 +63,10 @@ EXPORTS = {
     "kw_gemv": (ctypes.c_int, [ctypes.POINTER(GemmArgs), c_vp]),
     "kw_pack_weight": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "kw_packed_weight_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
+    "kw_gemv_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64, c_i64]),
     "kw_layernorm": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp]),
     "kw_attention": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kw_self_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
                                          c_vp, c_vp]),
     "kw_cross_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,

@@ -40,6 +40,12 @@ class DecodeSession:
         self.logits = torch.empty((B, s.vocab_size), device=dev, dtype=torch.float32)
         self._bufs = {}
         self._plans = {}
+        # split-K scratch shared by every skinny GEMM of a step (stream-ordered; zeroed once)
+        ws = 0
+        if eng.packed:
+            for n_, k_ in ((3 * d, d), (d, d), (s.decoder_ffn_dim, d), (d, s.decoder_ffn_dim), (s.vocab_size, d)):
+                ws = max(ws, ops.gemv_workspace_bytes(B, n_, k_))
+        self.gemv_ws = torch.zeros(((ws + 3) // 4,), device=dev, dtype=torch.float32) if ws else None
         self._graph = None
         self._graph_key = None
         if enc is not None:
@@ -60,13 +66,19 @@ class DecodeSession:
                 attn=torch.empty((rows, d), device=dev, dtype=dt),
                 qx=torch.empty((rows, d), device=dev, dtype=dt),
                 ffn=torch.empty((rows, s.decoder_ffn_dim), device=dev, dtype=dt),
-                ws=torch.empty((ops.cross_attn_workspace_bytes(self.B, q, self.eng.H, _HD, self.T) // 4 + 1,),
+                # cross-attention partials + arrival counters (must start zeroed; kernels leave them zeroed)
+                ws=torch.zeros((ops.cross_attn_workspace_bytes(self.B, q, self.eng.H, _HD, self.T) // 4 + 1,),
                                device=dev, dtype=torch.float32),
+                # per-row LayerNorm statistics: (sum, sum of squares) per 16-column slot of h
+                stats=torch.zeros((rows * ((d + 15) // 16) * 2,), device=dev, dtype=torch.float32),
             )
         return self._bufs[q]
 
-    def _gemm(self, A, W, C, M, N, K, **kw):
-        """Row-chunked skinny GEMM (kw_gemv handles M <= 128) or the f32 GEMM in parity mode."""
+    def _gemm(self, A, W, C, M, N, K, ln=None, stats_out=None, **kw):
+        """Row-chunked skinny GEMM (kw_gemv handles M <= 128) or the f32 GEMM in parity mode.
+
+        ``ln`` = (h, stats, slots, eps): fused LayerNorm prologue (gamma/beta folded into W, bias at load);
+        ``stats_out``: statistics epilogue."""
         eng = self.eng
         if not eng.packed:
             return [ops.GemmPlan(A, W, C, M, N, K, **kw)]
@@ -74,10 +86,18 @@ class DecodeSession:
         lda = kw.pop("lda", K)
         ldc = kw.pop("ldc", N)
         a_off = kw.pop("a_offset", 0)
-        for m0 in range(0, M, 128):
-            mm = min(128, M - m0)
+        ncb = (N + 15) // 16
+        chunk = 128  # kw_gemv limit (it launches 32-row chunks itself)
+        for m0 in range(0, M, chunk):
+            mm = min(chunk, M - m0)
+            lnc = None
+            if ln is not None:
+                h, st, slots, eps = ln
+                lnc = (h, st[m0 * slots * 2:], slots, eps)
+            so = stats_out[m0 * ncb * 2:] if stats_out is not None else None
             plans.append(ops.GemmPlan(A, W, C, mm, N, K, lda=lda, ldc=ldc, a_offset=a_off + m0 * lda,
-                                      c_offset=m0 * ldc, packed=True, dtype=torch.bfloat16, **kw))
+                                      c_offset=m0 * ldc, packed=True, dtype=torch.bfloat16, ln=lnc, stats_out=so,
+                                      workspace=self.gemv_ws, **kw))
         return plans
 
     def _step_plans(self, q: int):
@@ -90,20 +110,46 @@ class DecodeSession:
         rows = B * q
         scale = _HD ** -0.5
         eps = s.layer_norm_eps
-        seq = [("embed", q, b["h"])]
-        for li, lay in enumerate(eng.dec_layers):
-            seq.append(("ln", b["h"], lay["ln1_g"], lay["ln1_b"], b["x"]))
-            seq += self._gemm(b["x"], lay["qkv_w"], b["qkv"], rows, 3 * d, d, bias=lay["qkv_b"], scale=scale, scale_cols=d)
-            seq.append(("self", q, b["qkv"], li, b["attn"]))
-            seq += self._gemm(b["attn"], lay["o_w"], b["h"], rows, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID)
-            seq.append(("ln", b["h"], lay["ln2_g"], lay["ln2_b"], b["x"]))
-            seq += self._gemm(b["x"], lay["xq_w"], b["qx"], rows, d, d, bias=lay["xq_b"], scale=scale, scale_cols=d)
-            seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
-            seq += self._gemm(b["attn"], lay["xo_w"], b["h"], rows, d, d, bias=lay["xo_b"], epilogue=L.KW_EPI_RESID)
-            seq.append(("ln", b["h"], lay["ln3_g"], lay["ln3_b"], b["x"]))
-            seq += self._gemm(b["x"], lay["fc1_w"], b["ffn"], rows, s.decoder_ffn_dim, d, bias=lay["fc1_b"], gelu=True)
-            seq += self._gemm(b["ffn"], lay["fc2_w"], b["h"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
-                              epilogue=L.KW_EPI_RESID)
+        if eng.packed:
+            # bf16 path: every decoder LayerNorm is fused into the GEMM that consumes it; its row statistics
+            # come from the embedding / residual-add epilogue that produced h.
+            st = b["stats"]
+            full = (d + 15) // 16
+            seq = [("embed", q, b["h"], st)]
+            slots = 1
+            for li, lay in enumerate(eng.dec_layers):
+                seq += self._gemm(b["x"], lay["qkv_w"], b["qkv"], rows, 3 * d, d, bias=lay["qkv_b"], scale=scale,
+                                  scale_cols=d, ln=(b["h"], st, slots, eps))
+                seq.append(("self", q, b["qkv"], li, b["attn"]))
+                seq += self._gemm(b["attn"], lay["o_w"], b["h"], rows, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID,
+                                  stats_out=st)
+                seq += self._gemm(b["x"], lay["xq_w"], b["qx"], rows, d, d, bias=lay["xq_b"], scale=scale, scale_cols=d,
+                                  ln=(b["h"], st, full, eps))
+                seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
+                seq += self._gemm(b["attn"], lay["xo_w"], b["h"], rows, d, d, bias=lay["xo_b"], epilogue=L.KW_EPI_RESID,
+                                  stats_out=st)
+                seq += self._gemm(b["x"], lay["fc1_w"], b["ffn"], rows, s.decoder_ffn_dim, d, bias=lay["fc1_b"],
+                                  gelu=True, ln=(b["h"], st, full, eps))
+                seq += self._gemm(b["ffn"], lay["fc2_w"], b["h"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
+                                  epilogue=L.KW_EPI_RESID, stats_out=st)
+                slots = full
+        else:
+            seq = [("embed", q, b["h"], None)]
+            for li, lay in enumerate(eng.dec_layers):
+                seq.append(("ln", b["h"], lay["ln1_g"], lay["ln1_b"], b["x"]))
+                seq += self._gemm(b["x"], lay["qkv_w"], b["qkv"], rows, 3 * d, d, bias=lay["qkv_b"], scale=scale,
+                                  scale_cols=d)
+                seq.append(("self", q, b["qkv"], li, b["attn"]))
+                seq += self._gemm(b["attn"], lay["o_w"], b["h"], rows, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID)
+                seq.append(("ln", b["h"], lay["ln2_g"], lay["ln2_b"], b["x"]))
+                seq += self._gemm(b["x"], lay["xq_w"], b["qx"], rows, d, d, bias=lay["xq_b"], scale=scale, scale_cols=d)
+                seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
+                seq += self._gemm(b["attn"], lay["xo_w"], b["h"], rows, d, d, bias=lay["xo_b"], epilogue=L.KW_EPI_RESID)
+                seq.append(("ln", b["h"], lay["ln3_g"], lay["ln3_b"], b["x"]))
+                seq += self._gemm(b["x"], lay["fc1_w"], b["ffn"], rows, s.decoder_ffn_dim, d, bias=lay["fc1_b"],
+                                  gelu=True)
+                seq += self._gemm(b["ffn"], lay["fc2_w"], b["h"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
+                                  epilogue=L.KW_EPI_RESID)
         seq.append(("ln", b["h"], eng.dec_ln_g, eng.dec_ln_b, b["x"]))
         # LM head on the last position of every row (proj_out tied to embed_tokens, f32 logits)
         seq += self._gemm(b["x"], eng.lm_w, self.logits, B, s.vocab_size, d, lda=q * d, a_offset=(q - 1) * d)
@@ -121,7 +167,7 @@ class DecodeSession:
             if k == "ln":
                 ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4])
             elif k == "embed":
-                ops.embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2])
+                ops.embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2], p[3])
             elif k == "self":
                 _, q, qkv, li, out = p
                 ops.self_attn_step(qkv, B, q, H, _HD, self.kc[li], self.vc[li], T_MAX, self.cur_len, out)

@@ -123,24 +123,35 @@ class WhisperEngine:
         pk = ops.pack_weight if packed else (lambda w: w)
         self.dec_layers = []
         ckv_w, ckv_b = [], []
+        def fold(w, b, ln):
+            """Packed (bf16) path: the LayerNorm feeding this projection is fused into kw_gemv, which forms
+            only (h - mean) * rstd; gamma/beta are folded here: W' = W diag(gamma), b' = b + W beta."""
+            if not packed:
+                return pk(self._dev(w)), self._dev(b, f32)
+            gam, bet = g(f"{ln}.weight").float(), g(f"{ln}.bias").float()
+            w32 = w.float()
+            return pk(self._dev(w32 * gam[None, :])), self._dev(b.float() + w32 @ bet, f32)
+
         for i in range(s.decoder_layers):
             p = f"model.decoder.layers.{i}"
-            qkv_w, qkv_b = attn_qkv(f"{p}.self_attn")
+            qkv_w, qkv_b = fold(*attn_qkv(f"{p}.self_attn"), f"{p}.self_attn_layer_norm")
+            xq_w, xq_b = fold(g(f"{p}.encoder_attn.q_proj.weight"), g(f"{p}.encoder_attn.q_proj.bias"),
+                              f"{p}.encoder_attn_layer_norm")
+            fc1_w, fc1_b = fold(g(f"{p}.fc1.weight"), g(f"{p}.fc1.bias"), f"{p}.final_layer_norm")
             lay = dict(
                 ln1_g=self._dev(g(f"{p}.self_attn_layer_norm.weight"), f32),
                 ln1_b=self._dev(g(f"{p}.self_attn_layer_norm.bias"), f32),
-                qkv_w=pk(self._dev(qkv_w)), qkv_b=self._dev(qkv_b, f32),
+                qkv_w=qkv_w, qkv_b=qkv_b,
                 o_w=pk(self._dev(g(f"{p}.self_attn.out_proj.weight"))),
                 o_b=self._dev(g(f"{p}.self_attn.out_proj.bias"), f32),
                 ln2_g=self._dev(g(f"{p}.encoder_attn_layer_norm.weight"), f32),
                 ln2_b=self._dev(g(f"{p}.encoder_attn_layer_norm.bias"), f32),
-                xq_w=pk(self._dev(g(f"{p}.encoder_attn.q_proj.weight"))),
-                xq_b=self._dev(g(f"{p}.encoder_attn.q_proj.bias"), f32),
+                xq_w=xq_w, xq_b=xq_b,
                 xo_w=pk(self._dev(g(f"{p}.encoder_attn.out_proj.weight"))),
                 xo_b=self._dev(g(f"{p}.encoder_attn.out_proj.bias"), f32),
                 ln3_g=self._dev(g(f"{p}.final_layer_norm.weight"), f32),
                 ln3_b=self._dev(g(f"{p}.final_layer_norm.bias"), f32),
-                fc1_w=pk(self._dev(g(f"{p}.fc1.weight"))), fc1_b=self._dev(g(f"{p}.fc1.bias"), f32),
+                fc1_w=fc1_w, fc1_b=fc1_b,
                 fc2_w=pk(self._dev(g(f"{p}.fc2.weight"))), fc2_b=self._dev(g(f"{p}.fc2.bias"), f32),
             )
             self.dec_layers.append(lay)

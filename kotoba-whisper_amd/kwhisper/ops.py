@@ -87,9 +87,11 @@ class GemmPlan:
     def __init__(self, A, W, C, M, N, K, *, bias=None, lda=None, a_rows_per_batch=0, a_batch_stride=0,
                  ldc=None, c_rows_per_batch=0, c_batch_stride=0, epilogue=L.KW_EPI_STORE, gelu=False,
                  scale=1.0, scale_cols=0, row_add=None, row_add_period=0, hs_seq=0, hs_heads=0, hs_head_dim=0,
-                 packed=False, dtype=None, a_offset=0, c_offset=0):
-        _cuda(A, W, C, bias, row_add)
-        self._keep = (A, W, C, bias, row_add)
+                 packed=False, dtype=None, a_offset=0, c_offset=0, ln=None, stats_out=None, workspace=None):
+        """``ln`` = (h f32 [M][K], stats [M][slots][2], slots, eps): fused LayerNorm prologue
+        (kw_gemv only; A is then ignored; the LayerNorm's gamma/beta must be folded into W and bias).  ``stats_out``: row statistics epilogue (RESID only)."""
+        _cuda(A, W, C, bias, row_add, stats_out)
+        self._keep = (A, W, C, bias, row_add, ln, stats_out)
         dt = _dt(W) if dtype is None else _DT[dtype]
         a = L.GemmArgs()
         a.dtype = dt
@@ -112,6 +114,24 @@ class GemmPlan:
         a.row_add = row_add.data_ptr() if row_add is not None else None
         a.row_add_period = row_add_period
         a.hs_seq, a.hs_heads, a.hs_head_dim = hs_seq, hs_heads, hs_head_dim
+        if ln is not None:
+            h, st, slots, eps = ln
+            _cuda(h, st)
+            a.ln_h = h.data_ptr() + a_offset * h.element_size()
+            a.ln_stats = st.data_ptr()
+            a.ln_slots = slots
+            a.ln_eps = float(eps)
+        if stats_out is not None:
+            a.stats_out = stats_out.data_ptr()
+        if packed:
+            need = gemv_workspace_bytes(M, N, K)
+            if workspace is None:
+                workspace = torch.zeros((need + 3) // 4, device=W.device, dtype=torch.float32)
+            if workspace.numel() * workspace.element_size() < need:
+                raise ValueError("gemv workspace too small")
+            a.workspace = workspace.data_ptr()
+            a.ws_bytes = workspace.numel() * workspace.element_size()
+            self._keep = self._keep + (workspace,)
         if bias is not None and bias.dtype != torch.float32:
             raise ValueError("bias must be float32")
         if row_add is not None and row_add.dtype != torch.float32:
@@ -124,6 +144,10 @@ class GemmPlan:
 
     def __call__(self):
         L.check(self._fn(self._ref, _s()), self._name)
+
+
+def gemv_workspace_bytes(M: int, N: int, K: int) -> int:
+    return int(_lib().kw_gemv_workspace_bytes(M, N, K))
 
 
 def pack_weight(W: torch.Tensor) -> torch.Tensor:
@@ -146,10 +170,10 @@ def attention(qkv: torch.Tensor, B: int, H: int, T: int, hd: int, out: torch.Ten
     return out
 
 
-def embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h):
-    _cuda(ids, cur_len, tok_emb, pos_emb, h)
+def embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h, stats_out=None):
+    _cuda(ids, cur_len, tok_emb, pos_emb, h, stats_out)
     L.check(_lib().kw_embed(_dt(tok_emb), _p(ids), ids.stride(0), B, q_len, _p(cur_len), _p(tok_emb), _p(pos_emb),
-                            tok_emb.shape[1], _p(h), _s()), "kw_embed")
+                            tok_emb.shape[1], _p(h), _p(stats_out), _s()), "kw_embed")
 
 
 def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out):

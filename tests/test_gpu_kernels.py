@@ -251,7 +251,7 @@ def test_cross_attn_step(dtype, q_len, S):
     v = torch.randn(B, H, S, hd, device="cuda").to(dtype)
     q = (torch.randn(B * q_len, d, device="cuda") * 0.3).to(dtype)
     out = torch.empty(B * q_len, d, device="cuda", dtype=dtype)
-    ws = torch.empty(ops.cross_attn_workspace_bytes(B, q_len, H, hd, S) // 4 + 1, device="cuda")
+    ws = torch.zeros(ops.cross_attn_workspace_bytes(B, q_len, H, hd, S) // 4 + 1, device="cuda")
     ops.cross_attn_step(q, B, q_len, H, hd, k, v, S, out, ws)
     qq = q.float().view(B, q_len, H, hd).permute(0, 2, 1, 3)
     ref = (torch.softmax(qq @ k.float().transpose(-1, -2), -1) @ v.float()).permute(0, 2, 1, 3).reshape(B * q_len, d)
@@ -313,3 +313,56 @@ def test_greedy_step_vs_oracle(rt, n_hist):
         assert tok[b] == exp_tok
     assert int(cur.item()) == L_now + 1
     assert int(nun.item()) == int(unf.sum().item())
+
+
+@pytest.mark.parametrize("ksplit", [None, "4"])
+@pytest.mark.parametrize("M", [32, 5, 70])
+def test_gemv_fused_layernorm_and_stats(monkeypatch, ksplit, M):
+    """LayerNorm prologue from producer statistics (gamma/beta folded into W and bias, as the engine
+    loads them) + residual-statistics epilogue (decode fusion); with and without the K-split seam."""
+    if ksplit:
+        monkeypatch.setenv("KW_GEMV_KSPLIT", ksplit)
+    d, N = 1280, 3840
+    h = torch.randn(M, d, device="cuda") * 2 + 0.5
+    g = 1 + 0.1 * torch.randn(d, device="cuda")
+    bb = 0.1 * torch.randn(d, device="cuda")
+    # producer statistics with 80 slots of 16 columns
+    st = torch.stack([h.view(M, 80, 16).sum(-1), (h.view(M, 80, 16) ** 2).sum(-1)], -1).contiguous()
+    W = (torch.randn(N, d, device="cuda") / d ** 0.5).bfloat16()
+    bias = torch.randn(N, device="cuda")
+    Wp = ops.pack_weight((W.float() * g[None, :]).bfloat16())
+    bias_f = bias + W.float() @ bb
+    C = torch.empty(M, N, device="cuda")
+    dummy = torch.empty(M, d, device="cuda", dtype=torch.bfloat16)
+    ops.GemmPlan(dummy, Wp, C, M, N, d, bias=bias_f, packed=True, dtype=torch.bfloat16,
+                 ln=(h, st.view(-1), 80, 1e-5))()
+    xn = torch.nn.functional.layer_norm(h, (d,), g, bb, 1e-5).bfloat16()
+    torch.testing.assert_close(C, _ref_gemm(xn, W, bias), atol=3e-2, rtol=2e-2)
+    # statistics epilogue: h2 = h + A.W2^T + b2 ; stats of h2 per 16-col slot
+    W2 = (torch.randn(d, N, device="cuda") / N ** 0.5).bfloat16()
+    b2 = torch.randn(d, device="cuda")
+    A2 = torch.randn(M, N, device="cuda").bfloat16()
+    h2 = h.clone()
+    so = torch.zeros(M * 80 * 2, device="cuda")
+    ops.GemmPlan(A2, ops.pack_weight(W2), h2, M, d, N, bias=b2, packed=True, dtype=torch.bfloat16,
+                 epilogue=L.KW_EPI_RESID, stats_out=so)()
+    ref = h + _ref_gemm(A2, W2, b2)
+    torch.testing.assert_close(h2, ref, atol=2e-3, rtol=2e-3)
+    so = so.view(M, 80, 2)
+    torch.testing.assert_close(so[..., 0], h2.view(M, 80, 16).sum(-1), atol=1e-3, rtol=1e-4)
+    torch.testing.assert_close(so[..., 1], (h2.view(M, 80, 16) ** 2).sum(-1), atol=1e-2, rtol=1e-4)
+
+
+def test_embed_stats():
+    B, q, d, V = 3, 2, 384, 1000
+    tok = torch.randn(V, d, device="cuda").bfloat16()
+    pos = torch.randn(448, d, device="cuda").bfloat16()
+    ids = torch.randint(0, V, (B, 449), device="cuda")
+    cur = torch.tensor([7], dtype=torch.int32, device="cuda")
+    h = torch.empty(B * q, d, device="cuda")
+    st = torch.empty(B * q * 2, device="cuda")
+    ops.embed(ids, B, q, cur, tok, pos, h, st)
+    ref = (tok[ids[:, 5:7]].float() + pos[5:7].float()).reshape(B * q, d)
+    torch.testing.assert_close(h, ref)
+    torch.testing.assert_close(st.view(-1, 2)[:, 0], ref.sum(-1), atol=1e-3, rtol=1e-5)
+    torch.testing.assert_close(st.view(-1, 2)[:, 1], (ref ** 2).sum(-1), atol=1e-2, rtol=1e-5)

@@ -1,0 +1,106 @@
+#!/usr/bin/env python
+"""Decode-kernel microbenchmarks on the MI355X (development tool, not part of the product path).
+
+Times each decode-step kernel at large-v3 shapes (B=32) cycling over 32 distinct weight / K-V
+buffers (as the 32 decoder layers do) so the 256 MB Infinity Cache cannot serve repeats.
+
+    python tools/kbench.py [--reps 20]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kotoba-whisper_amd"))
+
+import torch  # noqa: E402
+
+from kwhisper import _lib as L  # noqa: E402
+from kwhisper import ops  # noqa: E402
+
+
+def timeit(fns, reps):
+    """Device time per launch: the launches are captured once into a hipGraph and replayed, so host
+    launch overhead is excluded (kernel boundaries are included, as in the decode step)."""
+    for f in fns:
+        f()
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(g, stream=side):
+        for f in fns:
+            f()
+    torch.cuda.current_stream().wait_stream(side)
+    g.replay()
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        g.replay()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / (reps * len(fns))  # us per launch
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--layers", type=int, default=32)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    B, d, H, S, F = 32, 1280, 20, 1500, 5120
+    nl = a.layers
+    res = {"variant": os.environ.get("KW_GEMV_VARIANT", "0")}
+    h = torch.randn(B, d, device=dev)
+    st = torch.stack([h.view(B, 80, 16).sum(-1), (h.view(B, 80, 16) ** 2).sum(-1)], -1).contiguous().view(-1)
+    g = torch.ones(d, device=dev)
+    bb = torch.zeros(d, device=dev)
+    x = torch.randn(B, F, device=dev).bfloat16()
+    for name, N, K, lna, resid in [("qkv_ln", 3 * d, d, True, False), ("o_resid", d, d, False, True),
+                                   ("xq_ln", d, d, True, False), ("fc1_ln_gelu", F, d, True, False),
+                                   ("fc2_resid", d, F, False, True), ("o_plain", d, d, False, False),
+                                   ("lm_head", 51866, d, False, False)]:
+        n_bufs = 1 if name == "lm_head" else nl
+        Ws = [ops.pack_weight((torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()) for _ in range(n_bufs)]
+        bias = torch.zeros(N, device=dev)
+        C = torch.empty(B, N, device=dev) if (resid or name == "lm_head") else torch.empty(B, N, device=dev,
+                                                                                          dtype=torch.bfloat16)
+        so = torch.zeros(B * ((N + 15) // 16) * 2, device=dev) if resid else None
+        plans = []
+        for W in Ws:
+            kw = dict(bias=bias, packed=True, dtype=torch.bfloat16)
+            if lna:
+                kw["ln"] = (h, st, 80, 1e-5)
+            if resid:
+                kw.update(epilogue=L.KW_EPI_RESID, stats_out=so)
+            if name.startswith("fc1"):
+                kw["gelu"] = True
+            plans.append(ops.GemmPlan(x[:, :K].contiguous() if not lna else x[:, :K].contiguous(), W, C, B, N, K,
+                                      **kw))
+        us = timeit(plans, a.reps)
+        res[name] = {"us": round(us, 2), "GBps": round(N * K * 2 / us / 1e3, 1)}
+    # attention kernels
+    cross = [torch.randn(2, B, H, S, 64, device=dev).bfloat16() for _ in range(nl)]
+    q = torch.randn(B, d, device=dev).bfloat16()
+    out = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
+    ws = torch.zeros(ops.cross_attn_workspace_bytes(B, 1, H, 64, S) // 4 + 1, device=dev)
+    fns = [lambda c=c: ops.cross_attn_step(q, B, 1, H, 64, c[0], c[1], S, out, ws) for c in cross]
+    us = timeit(fns, max(1, a.reps // 4))
+    res["cross_attn"] = {"us": round(us, 2), "GBps": round(2 * B * H * S * 64 * 2 / us / 1e3, 1)}
+    del cross
+    kc = torch.randn(nl, B, H, 448, 64, device=dev).bfloat16()
+    vc = torch.randn(nl, B, H, 448, 64, device=dev).bfloat16()
+    qkv = torch.randn(B, 3 * d, device=dev).bfloat16()
+    cur = torch.tensor([132], dtype=torch.int32, device=dev)
+    fns = [lambda i=i: ops.self_attn_step(qkv, B, 1, H, 64, kc[i], vc[i], 448, cur, out) for i in range(nl)]
+    res["self_attn_t132"] = {"us": round(timeit(fns, a.reps), 2)}
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
