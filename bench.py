@@ -33,6 +33,24 @@ BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA spec
 ENC_FLOP_PER_CLIP = 2.2738e12
 
 
+def pmc_traffic(kernel: str):
+    """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 FETCH_SIZE summary
+    (profiles/rNN_pmc_fetch.csv, written by tools/profile.sh + tools/rocpd_summary.py): FETCH_SIZE is
+    in KB and counts half the bytes of 16-B/lane streaming reads on gfx950 (MI355X_MICROARCH.md
+    section HBM), hence x 1024 x 2.  Returns (bytes, source) or (None, None)."""
+    import csv
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch.csv")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        for row in csv.DictReader(f):
+            if row["Counter"] == "FETCH_SIZE" and kernel in row["Name"]:
+                return float(row["Mean"]) * 1024 * 2, os.path.relpath(files[-1], ROOT) + " (FETCH_SIZE KB x1024 x2)"
+    return None, None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -170,6 +188,9 @@ def main():
                          "frac": ENC_FLOP_PER_CLIP * B / enc_t / 1e12 / BF16_PEAK_TFLOPS},
         "decode_step_ms": step_t * 1e3 if step_t else None,
     }
+    traffic, src = pmc_traffic("cross_attn_kernel")
+    result["roofline"]["traffic"] = traffic
+    result["roofline"]["traffic_source"] = src
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle.cpu_baseline import hf_cpu_generate_rate
 

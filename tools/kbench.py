@@ -22,12 +22,21 @@ from kwhisper import _lib as L  # noqa: E402
 from kwhisper import ops  # noqa: E402
 
 
+EAGER = False
+
+
 def timeit(fns, reps):
     """Device time per launch: the launches are captured once into a hipGraph and replayed, so host
     launch overhead is excluded (kernel boundaries are included, as in the decode step)."""
     for f in fns:
         f()
     torch.cuda.synchronize()
+    if EAGER:  # plain launches (for PMC passes: one counter record per dispatch)
+        for _ in range(reps):
+            for f in fns:
+                f()
+        torch.cuda.synchronize()
+        return float("nan")
     g = torch.cuda.CUDAGraph()
     side = torch.cuda.Stream()
     side.wait_stream(torch.cuda.current_stream())
@@ -51,7 +60,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--only", default="", help="comma list of kernel names to run (default: all)")
+    ap.add_argument("--eager", action="store_true", help="no graph, no timing (for rocprofv3 --pmc passes)")
     a = ap.parse_args()
+    global EAGER
+    EAGER = a.eager
+    only = set(filter(None, a.only.split(",")))
+    want = lambda n: not only or n in only  # noqa: E731
     dev = torch.device("cuda")
     B, d, H, S, F = 32, 1280, 20, 1500, 5120
     nl = a.layers
@@ -65,6 +80,8 @@ def main():
                                    ("xq_ln", d, d, True, False), ("fc1_ln_gelu", F, d, True, False),
                                    ("fc2_resid", d, F, False, True), ("o_plain", d, d, False, False),
                                    ("lm_head", 51866, d, False, False)]:
+        if not want(name):
+            continue
         n_bufs = 1 if name == "lm_head" else nl
         Ws = [ops.pack_weight((torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()) for _ in range(n_bufs)]
         bias = torch.zeros(N, device=dev)
@@ -85,6 +102,9 @@ def main():
         us = timeit(plans, a.reps)
         res[name] = {"us": round(us, 2), "GBps": round(N * K * 2 / us / 1e3, 1)}
     # attention kernels
+    if not want("cross_attn") and not want("self_attn_t132"):
+        print(json.dumps(res))
+        return
     cross = [torch.randn(2, B, H, S, 64, device=dev).bfloat16() for _ in range(nl)]
     q = torch.randn(B, d, device=dev).bfloat16()
     out = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
