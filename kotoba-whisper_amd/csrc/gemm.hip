@@ -13,6 +13,8 @@
 //    come from L2; 4 waves split K and reduce through LDS.  HBM-bound (weights read once per step).
 // Shared epilogues: bias, exact GELU, column scale (q * head_dim^-0.5, modeling_whisper.py:309),
 // row-periodic add (encoder positions, :621-624), residual add into the f32 stream, head-split store.
+#include <stdlib.h>
+
 #include "gemm_common.h"
 
 namespace {
@@ -125,6 +127,227 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmP p) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// bf16 256x256x64 ping-pong (encoder GEMMs, cross-K/V projection)
+//
+// 8 waves in two groups of four (one wave of each group per SIMD).  Group g owns output rows
+// g*128..+128; wave q of a group owns columns q*64..+64 (8x4 tiles of v_mfma_f32_16x16x32_bf16,
+// 128 accumulator registers).  The groups run one barrier apart, so on every SIMD one wave issues its
+// LDS fragment reads while the other runs its 64-MFMA cluster.  LDS holds two K-tile buffers of
+// 64 KB (A image + W image, 256 rows x 128 B, XOR-swizzled on the SOURCE address so the lane-linear
+// global_load_lds image reads conflict-free).  Group 0 stages A, group 1 stages W; every staged tile
+// has two barrier slots to land and is retired by the issuing wave's vmcnt before the barrier that
+// precedes its first read (raw s_barrier: no implicit vmcnt(0) drain).
+//
+// Slot s = interval between two consecutive hardware barriers.  Slot 2t: group 0 reads tile t,
+// group 1 multiplies tile t-1.  Slot 2t+1: group 0 multiplies tile t, group 1 reads tile t.  Every
+// reader drains its LDS reads (lgkmcnt(0)) before the barrier that ends its read slot.  Group 0
+// stages A of tile t+1 in slot 2t (tile t-1's buffer, last read in slot 2t-1) and retires it at the end
+// of slot 2t+1; group 1 stages W of tile t+2 in slot 2t+1 after its own reads of tile t (group 0 read
+// tile t in slot 2t) and retires it at the end of slot 2t+3.  Both are read from slot 2t+2 / 2t+4 on.
+//
+// Epilogue: each wave stages its 128x64 f32 results through a private 17 KB LDS region (64 rows at a
+// time, 272-B padded rows: conflict-free b32 writes) and stores 16-B (f32) / 8-B (bf16) row pieces,
+// so every wave store instruction covers 4 rows x 64 contiguous columns.
+// ------------------------------------------------------------------------------------------------
+constexpr int PB = 256, PK = 64;
+constexpr int P_OP = PB * PK * 2;  // 32 KB: one operand image of one K-tile
+constexpr int P_BUF = 2 * P_OP;    // 64 KB
+constexpr int P_LDS = 2 * P_BUF;   // 128 KB of K-tile buffers
+constexpr int P_EPI = 64 * 68 * 4; // per-wave epilogue region (64 padded f32 rows)
+constexpr int P_LDS_ALLOC = P_LDS > 8 * P_EPI ? P_LDS : 8 * P_EPI;  // 136 KB
+
+__device__ __forceinline__ void pp_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
+
+template <int EPI, typename TC>
+__global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, wq = wave & 3;
+
+  const int tiles_n = p.N / PB;
+  const int tiles_m = (p.M + PB - 1) / PB;
+  const int nwg = tiles_m * tiles_n;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const char* sbase = grp == 0 ? reinterpret_cast<const char*>(p.A) : reinterpret_cast<const char*>(p.W);
+  uint32_t soff[8];
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;  // bijective XCD remap: each XCD a contiguous tile run
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
+  const int tm = wgid / tiles_n, tn = wgid - tm * tiles_n;
+  const int m0 = tm * PB, n0 = tn * PB;
+  // staging sources: group 0 -> A rows m0.., group 1 -> W rows n0..; 8 x 1 KB glds per wave per K-tile
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = 8 * (wq * 8 + i) + (lane >> 3);
+    const int c = (lane & 7) ^ ((r >> 1) & 7);
+    if (grp == 0) {
+      const int m = min(m0 + r, p.M - 1);
+      soff[i] = (uint32_t)((row_off(m, p.a_rpb, p.a_bs, p.lda) + c * 8) * 2);
+    } else {
+      soff[i] = (uint32_t)(((int64_t)(n0 + r) * p.K + c * 8) * 2);
+    }
+  }
+  auto stage = [&](int t, int buf) {
+    char* dst = smem + buf * P_BUF + grp * P_OP + wq * 8 * 1024;
+    const char* src = sbase + (int64_t)t * (PK * 2);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) glds16(src + soff[i], dst + i * 1024);
+  };
+
+  // fragment read offsets (row = lane & 15 within a 16-row rep; the swizzle term (row >> 1) & 7 is per lane)
+  const int swz = (lane & 15) >> 1;
+  const int rd0 = (lane & 15) * 128 + (((0 * 4 + (lane >> 4)) ^ swz) << 4);
+  const int rd1 = (lane & 15) * 128 + (((1 * 4 + (lane >> 4)) ^ swz) << 4);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[8][2], b[4][2];
+
+  auto read_frags = [&](int buf) {
+    const char* As = smem + buf * P_BUF + grp * 128 * 128;
+    const char* Bs = smem + buf * P_BUF + P_OP + wq * 64 * 128;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      b[j][0] = *reinterpret_cast<const bf16x8*>(Bs + j * 2048 + rd0);
+      b[j][1] = *reinterpret_cast<const bf16x8*>(Bs + j * 2048 + rd1);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      a[i][0] = *reinterpret_cast<const bf16x8*>(As + i * 2048 + rd0);
+      a[i][1] = *reinterpret_cast<const bf16x8*>(As + i * 2048 + rd1);
+    }
+  };
+  auto mma = [&]() {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b[j][ks], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  const int nk = p.K / PK;
+  // prologue: tile 0 (both operands) and W of tile 1
+  stage(0, 0);
+  if (grp == 1 && nk > 1) stage(1, 1);
+  if (grp == 1 && nk > 1)
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  pp_barrier();
+  if (grp == 1) pp_barrier();  // the stagger
+
+  if (grp == 0) {
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      read_frags(buf);
+      if (t + 1 < nk) stage(t + 1, buf ^ 1);  // A of tile t+1 (its buffer's last reader finished in slot 2t-1)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();
+      mma();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A of tile t+1 landed
+      pp_barrier();
+    }
+    pp_barrier();  // balances group 1's stagger barrier
+  } else {
+    // group 1 stages W of tile t+2 in its own read slot, after its reads of tile t drained: group 0 read
+    // tile t one slot earlier, so the buffer is free; the W of tile t+1 (issued one read slot earlier)
+    // must have landed before this slot's barrier: vmcnt(8) leaves only the 8 just-issued pieces.
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      read_frags(buf);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (t + 2 < nk) {
+        stage(t + 2, buf);
+        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      pp_barrier();
+      mma();
+      pp_barrier();
+    }
+  }
+
+  // epilogue (LDS is free: every wave passed the last barrier, every glds retired)
+  float* ep = reinterpret_cast<float*>(smem + wave * P_EPI);
+  const int cq = lane & 15;                      // this lane's 4-column group within the wave's 64 columns
+  const int n = n0 + wq * 64 + 4 * cq;           // first of its 4 columns
+  float cb[4], cs[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    cb[e] = p.bias ? p.bias[n + e] : 0.f;
+    cs[e] = n + e < p.scale_cols ? p.scale : 1.f;
+  }
+  int64_t coff = n;
+  const int nb = p.M / p.hs_seq;
+  if constexpr (EPI == KW_EPI_HEADSPLIT) {
+    const int width = p.hs_heads * p.hs_hd;
+    const int part = n / width, rem = n - part * width;
+    const int h = rem / p.hs_hd, d = rem - h * p.hs_hd;
+    coff = ((int64_t)part * nb * p.hs_heads + h) * (int64_t)p.hs_seq * p.hs_hd + d;
+  }
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    // acc tiles i = 4*half .. 4*half+3 -> LDS rows 16*(i-4*half) + 4*(lane>>4) + r, column 16j + (lane&15)
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ep[(16 * ii + 4 * (lane >> 4) + r) * 68 + 16 * j + (lane & 15)] = acc[4 * half + ii][j][r];
+#pragma unroll 4
+    for (int q = 0; q < 16; ++q) {
+      const int rr = 4 * q + (lane >> 4);
+      const int m = m0 + grp * 128 + 64 * half + rr;
+      const float4 v4 = *reinterpret_cast<const float4*>(ep + rr * 68 + 4 * cq);
+      if (m >= p.M) continue;
+      float v[4] = {v4.x + cb[0], v4.y + cb[1], v4.z + cb[2], v4.w + cb[3]};
+      int64_t off;
+      if constexpr (EPI == KW_EPI_HEADSPLIT) {
+        const int bb = m / p.hs_seq, tt = m - bb * p.hs_seq;
+        off = (int64_t)bb * p.hs_heads * p.hs_seq * p.hs_hd + (int64_t)tt * p.hs_hd + coff;
+      } else {
+        const int bb = m / (int)p.c_rpb;
+        off = (int64_t)bb * p.c_bs + (int64_t)(m - bb * (int)p.c_rpb) * p.ldc + coff;
+      }
+      if constexpr (EPI == KW_EPI_RESID) {
+        float4* c = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off);
+        float4 o = *c;
+        o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+        *c = o;
+      } else {
+        const float* ra = p.row_add ? p.row_add + (int64_t)(m % p.row_add_period) * p.N + n : nullptr;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (p.gelu) v[e] = gelu_erf(v[e]);
+          v[e] *= cs[e];
+          if (ra) v[e] += ra[e];
+        }
+        if constexpr (sizeof(TC) == 4) {
+          *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
+        } else {
+          ushort4 o;
+          o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
+          *reinterpret_cast<ushort4*>(reinterpret_cast<bf16_t*>(p.C) + off) = o;
+        }
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // f32 64x64x16 (exact fp32 via v_mfma_f32_32x32x2_f32)
 // ------------------------------------------------------------------------------------------------
 constexpr int FBM = 64, FBN = 64, FBK = 16;
@@ -183,6 +406,42 @@ hipError_t launch_bf16(const GemmP& p, int epi, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int EPI, typename TC>
+hipError_t launch256_one(const GemmP& p, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm256_kernel<EPI, TC>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, P_LDS_ALLOC);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int nwg = ((p.M + PB - 1) / PB) * (p.N / PB);
+  hipLaunchKernelGGL((gemm256_kernel<EPI, TC>), dim3(nwg), dim3(512), P_LDS_ALLOC, s, p);
+  return hipGetLastError();
+}
+
+template <typename TC>
+hipError_t launch256(const GemmP& p, int epi, hipStream_t s) {
+  switch (epi) {
+    case KW_EPI_STORE: return launch256_one<KW_EPI_STORE, TC>(p, s);
+    case KW_EPI_RESID: return launch256_one<KW_EPI_RESID, float>(p, s);
+    default: return launch256_one<KW_EPI_HEADSPLIT, TC>(p, s);
+  }
+}
+
+// 256x256 ping-pong for the big GEMMs; KW_GEMM_TILE=128 (env) forces the 128x128 kernel (A/B runs).
+bool use256(const kw_gemm_args* a) {
+  static int forced = -1;
+  if (forced < 0) {
+    const char* e = getenv("KW_GEMM_TILE");
+    forced = (e && atoi(e) == 128) ? 1 : 0;
+  }
+  // 4-column vector epilogue: ldc, batch strides, head_dim and the C base 16-B aligned (f32) / 8-B (bf16)
+  const bool aligned = a->ldc % 4 == 0 && a->c_batch_stride % 4 == 0 && (a->hs_head_dim <= 0 || a->hs_head_dim % 4 == 0) &&
+                       ((uintptr_t)a->C % (a->c_dtype == KW_DT_F32 ? 16 : 8)) == 0;
+  return !forced && aligned && a->N % PB == 0 && a->M >= 4 * PB;
+}
+
 template <typename TC>
 hipError_t launch_f32(const GemmP& p, int epi, hipStream_t s) {
   dim3 grid((p.N + FBN - 1) / FBN, (p.M + FBM - 1) / FBM);
@@ -206,7 +465,10 @@ extern "C" int kw_gemm(const kw_gemm_args* a, kw_stream_t stream) {
   if (a->dtype == KW_DT_BF16) {
     if (a->N % BN != 0 || a->K % BK != 0 || a->lda % 8 != 0)
       return kw_set_error_msg(KW_EINVAL, "kw_gemm(bf16): needs N % 128 == 0, K % 64 == 0, lda % 8 == 0");
-    e = a->c_dtype == KW_DT_F32 ? launch_bf16<float>(p, a->epilogue, s) : launch_bf16<bf16_t>(p, a->epilogue, s);
+    if (use256(a))
+      e = a->c_dtype == KW_DT_F32 ? launch256<float>(p, a->epilogue, s) : launch256<bf16_t>(p, a->epilogue, s);
+    else
+      e = a->c_dtype == KW_DT_F32 ? launch_bf16<float>(p, a->epilogue, s) : launch_bf16<bf16_t>(p, a->epilogue, s);
   } else if (a->dtype == KW_DT_F32) {
     if (a->K % FBK != 0 || a->lda % 4 != 0)
       return kw_set_error_msg(KW_EINVAL, "kw_gemm(f32): needs K % 16 == 0, lda % 4 == 0");

@@ -88,6 +88,47 @@ def test_gemm_bf16_epilogues():
     torch.testing.assert_close(Hc, H0 + ref, atol=1e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("M,K", [(2000, 64), (2000, 128), (1100, 320), (4096, 1280)])
+def test_gemm256_pipeline_and_epilogues(M, K):
+    """The 256x256 ping-pong kernel (N % 256 == 0, M >= 1024): K-tile counts 1, 2, odd, 20; ragged last
+    row tile; STORE (gelu + column scale + row_add) and RESID epilogues."""
+    N = 512
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda")
+    ref = _ref_gemm(A, W, b)
+    ra = torch.randn(5, N, device="cuda")
+    C = torch.empty(M, N, device="cuda")
+    ops.GemmPlan(A, W, C, M, N, K, bias=b, gelu=True, scale=0.125, scale_cols=300, row_add=ra, row_add_period=5)()
+    r = torch.nn.functional.gelu(ref)
+    r[:, :300] *= 0.125
+    r += ra[torch.arange(M, device="cuda") % 5]
+    torch.testing.assert_close(C, r, atol=1e-3, rtol=1e-3)
+    H0 = torch.randn(M, N, device="cuda")
+    Hc = H0.clone()
+    ops.GemmPlan(A, W, Hc, M, N, K, bias=b, epilogue=L.KW_EPI_RESID)()
+    torch.testing.assert_close(Hc, H0 + ref, atol=1e-3, rtol=1e-3)
+    Cb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.GemmPlan(A, W, Cb, M, N, K, bias=b)()
+    torch.testing.assert_close(Cb.float(), ref, atol=2e-2, rtol=1e-2)
+
+
+def test_gemm256_headsplit():
+    B, T, H, hd = 3, 1500, 4, 64
+    d = H * hd
+    M, N, K = B * T, 3 * d, 256
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda")
+    C = torch.empty(3, B, H, T, hd, device="cuda", dtype=torch.bfloat16)
+    ops.GemmPlan(A, W, C, M, N, K, bias=b, epilogue=L.KW_EPI_HEADSPLIT, scale=0.125, scale_cols=d,
+                 hs_seq=T, hs_heads=H, hs_head_dim=hd)()
+    ref = _ref_gemm(A, W, b)
+    ref[:, :d] *= 0.125
+    ref = ref.view(B, T, 3, H, hd).permute(2, 0, 3, 1, 4)
+    torch.testing.assert_close(C.float(), ref, atol=2e-2, rtol=1e-2)
+
+
 def test_gemm_bf16_headsplit():
     B, T, H, hd = 2, 100, 2, 64
     d = H * hd
