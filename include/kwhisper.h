@@ -73,35 +73,66 @@ typedef struct {
   const float* row_add;      /* [period][N] f32 added after the activation, or NULL */
   int64_t row_add_period;
   int64_t hs_seq, hs_heads, hs_head_dim;
-  /* kw_gemv only -- fused LayerNorm prologue: if ln_h != NULL, A = (ln_h - mean) * rstd is formed on
-   * the fly (ln_h [M][K] f32, row pitch lda) from row statistics ln_stats [M][ln_slots][2] holding
-   * partial (sum, sum of squares) per slot, and ln_eps (modeling_whisper.py:434-446).  The
-   * LayerNorm's gamma/beta are NOT applied: fold them into the weights when loading them,
-   * W' = W diag(gamma), bias' = bias + W beta. */
-  const float* ln_h;
-  const float* ln_stats;
-  int64_t ln_slots;
-  float ln_eps;
-  /* kw_gemv RESID only: per-row (sum, sum of squares) of the UPDATED C over each 16-column block,
-   * written to stats_out[M][ceil(N/16)][2] -- the statistics of the next LayerNorm.  NULL = skip. */
-  float* stats_out;
-  /* kw_gemv split-K scratch (partial tiles + arrival counters): >= kw_gemv_workspace_bytes(M, N, K)
-   * bytes, ZERO-FILLED before first use (every call leaves the counters zero).  May be shared by all
-   * kw_gemv calls issued in order on one stream. */
-  void* workspace;
-  size_t ws_bytes;
 } kw_gemm_args;
 
 int kw_gemm(const kw_gemm_args* args, kw_stream_t stream);
 
-/* Skinny GEMM for decode steps (M <= 128): same contract as kw_gemm (STORE / RESID epilogues,
- * no row maps), W pre-packed by kw_pack_weight (bf16 only); optional fused LayerNorm prologue and
- * row-statistics epilogue (fields ln_* / stats_out above). */
-int kw_gemv(const kw_gemm_args* args, kw_stream_t stream);
-/* W [N][K] bf16 -> packed [ceil(N/16)][K/32][64 lanes][8] bf16 (rows >= N zero); K % 32 == 0. */
+/* ---- decode step (bf16 engine) ---------------------------------------------------------------
+ * Fixed-point LayerNorm statistics: a row's statistics are KW_LN_GROUPS pairs of int64
+ * (sum * 2^32, sum of squares * 2^28), added by independent producers (integer adds: the result is
+ * bitwise independent of their order); mean = sum(pairs.sum) / 2^32 / K, var = sum(pairs.sq) / 2^28 / K
+ * - mean^2.  Row pitch ld_stats (int64 elements, >= 2 * KW_LN_GROUPS). */
+#define KW_LN_GROUPS 8
+
+/* Decode-step linear over packed weights, any M (launched in 32-row chunks):
+ *   A = x (bf16 [M][ldx]) or, if ln_stats != NULL, the LayerNorm (x - mean) * rstd (eps ln_eps) of it,
+ *   with gamma/beta folded into W / bias by the caller (W' = W diag(gamma), b' = b + W beta) and
+ *   ln_colsum[n] = sum_k W'[n][k] (f32, of the bf16 values packed): computed as
+ *   rstd * (x W'^T - mean * ln_colsum)
+ *   (TF modeling_whisper.py:446,476,500 + 469-503, proj_out :1080);
+ *   STORE: C[m][n] = act(acc + bias) * (n < scale_cols ? scale : 1), C f32 or bf16;
+ *   RESID: h[m][n] += acc + bias (f32 residual, modeling_whisper.py:482,495,503), hb = bf16(h), and
+ *          optionally the next LayerNorm's fixed-point statistics added into stats_out.
+ * W: packed by kw_pack_weight.  workspace: >= kw_dec_linear_workspace_bytes(N, K) bytes, zero-filled
+ * before first use (calls leave it zeroed); one workspace may serve all calls on one stream. */
+typedef struct {
+  const void* x;
+  int64_t ldx;
+  const int64_t* ln_stats;   /* [M][ld_stats] or NULL */
+  int64_t ld_stats;
+  float ln_eps;
+  const float* ln_colsum;    /* [N], required with ln_stats */
+  const void* W;
+  const float* bias;         /* [N] f32 or NULL */
+  int epilogue;              /* KW_EPI_STORE or KW_EPI_RESID */
+  void* C;                   /* STORE output [M][ldc] */
+  int64_t ldc;
+  int c_dtype;
+  int gelu;
+  float scale;
+  int64_t scale_cols;
+  float* h;                  /* RESID: f32 residual [M][ldh] (in/out) */
+  void* hb;                  /* RESID: bf16 mirror [M][ldh] (out) */
+  int64_t ldh;
+  int64_t* stats_out;        /* RESID: [M][ld_stats] accumulators of the next LayerNorm, or NULL */
+  int64_t M, N, K;
+  void* workspace;
+  size_t ws_bytes;
+} kw_dec_linear_args;
+
+int kw_dec_linear(const kw_dec_linear_args* args, kw_stream_t stream);
+size_t kw_dec_linear_workspace_bytes(int64_t N, int64_t K);
+/* W [N][K] bf16 -> packed [ceil(N/32)*2][K/32][64 lanes][8] bf16 (columns >= N zero); K % 32 == 0. */
 int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed, kw_stream_t stream);
-size_t kw_gemv_workspace_bytes(int64_t M, int64_t N, int64_t K);
 size_t kw_packed_weight_bytes(int64_t N, int64_t K);
+
+/* Decode-step embedding for the bf16 engine: as kw_embed, plus hb = bf16(h), the first LayerNorm's
+ * statistics written to stats [B*q_len][ld_stats] (replacing, not adding), and n_zero int64 words
+ * at zero_stats set to 0 (the accumulators the step's later RESID linears add into). */
+int kw_dec_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
+                 const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
+                 void* hb, int64_t* stats, int64_t ld_stats, int64_t* zero_stats, int64_t n_zero,
+                 kw_stream_t stream);
 
 /* LayerNorm (eps) over the last dim of x [rows][dim] f32 -> y [rows][dim] (y_dtype);
  * TF modeling_whisper.py:371,377,434,443,446,642,790. dim % 4 == 0, dim <= 2048. */
@@ -117,8 +148,7 @@ int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, int64_t T, in
  * with L = *cur_len read on device (TF modeling_whisper.py:737-762; no embed scale). */
 int kw_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
              const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
-             float* stats_out, kw_stream_t stream);
-/* (stats_out: optional [B*q_len][1][2] row (sum, sum of squares) of h for a fused LayerNorm.) */
+             kw_stream_t stream);
 
 /* Decoder self-attention over a static cache (TF modeling_whisper.py:469-480, cache_utils.py:127-145):
  * appends k/v of the q_len newest positions [L-q_len, L) to k_cache/v_cache [B][H][t_max][hd],

@@ -1,0 +1,412 @@
+// Decode-step linear layers (a4/a5) over pre-packed weights, gfx950.
+//
+// One decode step multiplies B <= 32 rows (one token per sequence) by every decoder weight matrix:
+// q/k/v (modeling_whisper.py:469-480), out-proj, cross q / out-proj (:323-335), fc1 / fc2 (:499-503)
+// and the tied LM head proj_out (:1080).  At this size a linear is a weight STREAM: 3.3-13 MB per
+// matrix read once, ~2 k-tiles of MFMA work per 1 KB loaded.  The kernel is built for latency:
+//
+//  * weights pre-packed into 1-KB v_mfma_f32_16x16x32_bf16 B-fragments [N/16][K/32][64 lanes][8]
+//    (padded to a multiple of 32 columns), so every weight load is one coalesced 16-B/lane wave
+//    access; each wave issues ALL its weight and activation loads up front (KTM k-tiles x NCB column
+//    blocks, non-temporal weights) -- the kernel costs about one memory round trip plus transfer;
+//  * a workgroup owns NCB x 16 columns (NCB = 2 reuses each activation fragment twice); its waves
+//    split K and reduce through LDS; for few-column matrices with long K (fc2: N 1280, K 5120) KS
+//    workgroups split K with a deterministic seam (write-through partial slabs, an arrival counter,
+//    the last arriver sums the KS slabs in fixed order -- MI355X_MICROARCH "Valid forms" row 1);
+//  * fused LayerNorm: LN(x) W'^T = rstd * (x W'^T - mean * colsum(W')), so the MFMAs take the bf16
+//    residual mirror x as it is and the LayerNorm costs one multiply-add per output in the epilogue,
+//    with (mean, rstd) from per-row fixed-point statistics; gamma/beta are folded into W and bias at
+//    load time (W' = W diag(gamma), b' = b + W beta) and colsum(W') is precomputed per column;
+//  * RESID epilogue: h(f32) += acc + bias, the bf16 mirror hb = h for the next LayerNorm's operand,
+//    and the next LayerNorm's row statistics: every finishing column block adds its rows' (sum,
+//    sum of squares) as FIXED-POINT int64 (scales 2^32 / 2^28) into one of KW_LN_GROUPS accumulators
+//    per row.  Integer addition is associative, so the statistics -- and the tokens -- are bitwise
+//    deterministic whatever the workgroup order.
+#include <stdlib.h>
+
+#include "kw_common.h"
+
+namespace {
+
+constexpr int G = KW_LN_GROUPS;
+constexpr double S1 = 4294967296.0;  // 2^32: fixed-point scale of row sums
+constexpr double S2 = 268435456.0;   // 2^28: fixed-point scale of row sums of squares
+constexpr int CNT_MAX = 4096;        // seam arrival counters at the start of the workspace
+constexpr int MAXW = 8;              // waves per workgroup
+
+struct DecP {
+  const bf16_t* x;
+  int64_t ldx;
+  const int64_t* ln_stats;
+  int64_t ld_stats;
+  float ln_eps;
+  const float* ln_colsum;
+  const bf16x8* W;
+  const float* bias;
+  int epi;
+  void* C;
+  int64_t ldc;
+  int gelu;
+  float scale;
+  int scale_cols;
+  float* h;
+  bf16_t* hb;
+  int64_t ldh;
+  int64_t* stats_out;
+  int M, N, K;
+  float* slab;
+  int* cnt;
+};
+
+constexpr int KSMAX = 8;  // K splits per column group (host-checked)
+
+template <int KTM, int NCB, bool LNA, int EPI, typename TC>
+__global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
+  __shared__ f32x4 red[MAXW][NCB][2][64];
+  __shared__ float rstat[32][2];             // LayerNorm (mean, rstd) per row
+  __shared__ float tile[32][NCB * 16 + 1];   // RESID: the block's new h values, for row statistics
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int cg = blockIdx.x, ks = blockIdx.y;
+  const int nkt = p.K >> 5;
+  const int nsl = ksn * nw, sl = ks * nw + wave;
+  const int kt0 = (nkt * sl) / nsl, kt1 = (nkt * (sl + 1)) / nsl;  // <= KTM k-tiles (host-checked)
+  const int ktl = max(kt1 - 1, kt0);
+  const int M = p.M;
+  const int arow = lane & 15, akoff = 8 * (lane >> 4);
+  const int r0 = min(arow, M - 1), r1 = min(16 + arow, M - 1);
+
+  // 1. every load of this wave in flight: weights (non-temporal) and activations
+  bf16x8 w[NCB][KTM], a0[KTM], a1[KTM];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c)
+#pragma unroll
+    for (int u = 0; u < KTM; ++u)
+      w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)(cg * NCB + c) * nkt + min(kt0 + u, ktl)) * 64 + lane);
+#pragma unroll
+  for (int u = 0; u < KTM; ++u) {
+    const int k = min(kt0 + u, ktl) * 32 + akoff;
+    a0[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r0 * p.ldx + k);
+    a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
+  }
+  // LayerNorm statistics of the 32 rows (last wave: its loads queue behind the fewest weight loads... all
+  // waves issue the same count; wave nw-1 is as good as any) -> rstat in LDS
+  const bool stat_wave = LNA && wave == nw - 1 && lane < 32;
+  longlong2 stv[G];
+  if (stat_wave) {
+    const longlong2* sp = reinterpret_cast<const longlong2*>(p.ln_stats + (int64_t)min(lane, M - 1) * p.ld_stats);
+#pragma unroll
+    for (int g = 0; g < G; ++g) stv[g] = sp[g];
+  }
+  // epilogue operands of wave 0 (lane <-> column lane&15, rows 4*(lane>>4)+r and 16+...)
+  float hold[NCB][2][4];
+  if constexpr (EPI == KW_EPI_RESID) {
+    if (wave == 0) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = min(16 * hh + 4 * (lane >> 4) + r, M - 1);
+            hold[c][hh][r] = p.h[(int64_t)m * p.ldh + n];
+          }
+      }
+    }
+  }
+
+  // 2. MFMA over this wave's k-tiles (raw operand: the LayerNorm is applied in the epilogue)
+  f32x4 c0[NCB], c1[NCB];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    c0[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    c1[c] = c0[c];
+  }
+#pragma unroll
+  for (int u = 0; u < KTM; ++u) {
+    if (kt0 + u < kt1) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        c0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], w[c][u], c0[c], 0, 0, 0);
+        c1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[c][u], c1[c], 0, 0, 0);
+      }
+    }
+  }
+  if (stat_wave) {
+    int64_t sa = 0, sb = 0;
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      sa += stv[g].x;
+      sb += stv[g].y;
+    }
+    const double inv = 1.0 / p.K;
+    const double mean = (double)sa * (inv / S1);
+    const double var = fmax((double)sb * (inv / S2) - mean * mean, 0.0);
+    rstat[lane][0] = (float)mean;
+    rstat[lane][1] = rsqrtf((float)var + p.ln_eps);
+  }
+
+  // 3. reduce the waves' K slices (fixed order); wave 0 continues
+  if (nw > 1) {
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      red[wave][c][0][lane] = c0[c];
+      red[wave][c][1][lane] = c1[c];
+    }
+    __syncthreads();
+    if (wave != 0) return;
+    for (int w2 = 1; w2 < nw; ++w2)
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        c0[c] += red[w2][c][0][lane];
+        c1[c] += red[w2][c][1][lane];
+      }
+  }
+
+  // 4. K-split seam: publish the partial tile write-through, count arrivals, the last one sums in order
+  if (ksn > 1) {
+    float* mine = p.slab + ((int64_t)cg * ksn + ks) * (NCB * 512);
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __hip_atomic_store(mine + c * 512 + r * 64 + lane, c0[c][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(mine + c * 512 + 256 + r * 64 + lane, c1[c][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) {
+      const int prev = __hip_atomic_fetch_add(p.cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == ksn - 1;
+      if (last) __hip_atomic_store(p.cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    last = __shfl(last, 0, 64);
+    if (!last) return;
+    // every slab load in flight before the first add (fixed summation order q = 0, 1, ...)
+    const float* all = p.slab + (int64_t)cg * ksn * (NCB * 512);
+    float pv[KSMAX][NCB][8];
+#pragma unroll
+    for (int q = 0; q < KSMAX; ++q)
+#pragma unroll
+      for (int c = 0; c < NCB; ++c)
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          pv[q][c][e] = q < ksn ? __hip_atomic_load(all + q * NCB * 512 + c * 512 + (e >> 2) * 256 + (e & 3) * 64 + lane,
+                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                : 0.f;
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float v0 = pv[0][c][r], v1 = pv[0][c][4 + r];
+#pragma unroll
+        for (int q = 1; q < KSMAX; ++q) {
+          v0 += pv[q][c][r];
+          v1 += pv[q][c][4 + r];
+        }
+        c0[c][r] = v0;
+        c1[c][r] = v1;
+      }
+  }
+
+  // 5. epilogue: MFMA C layout -> element (row 4*(lane>>4)+r [+16], column lane&15)
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    const int cb = cg * NCB + c;
+    const int n = cb * 16 + (lane & 15);
+    const bool nvalid = n < p.N;
+    const float bn = (p.bias && nvalid) ? p.bias[n] : 0.f;
+    const float cs = (LNA && nvalid) ? p.ln_colsum[n] : 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * hh + 4 * (lane >> 4) + r;
+        const bool valid = nvalid && m < M;
+        float v = hh ? c1[c][r] : c0[c][r];
+        if constexpr (LNA) {  // LN(x) W'^T = rstd * (x W'^T - mean * colsum(W'))
+          const int mr = min(m, 31);
+          v = rstat[mr][1] * (v - rstat[mr][0] * cs);
+        }
+        v += bn;
+        if constexpr (EPI == KW_EPI_RESID) {
+          v += hold[c][hh][r];
+          if (valid) {
+            p.h[(int64_t)m * p.ldh + n] = v;
+            p.hb[(int64_t)m * p.ldh + n] = f2bf(v);
+          }
+          tile[m][c * 16 + (lane & 15)] = valid ? v : 0.f;
+        } else {
+          if (p.gelu) v = gelu_erf(v);
+          if (n < p.scale_cols) v *= p.scale;
+          if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
+        }
+      }
+    }
+  }
+  if constexpr (EPI == KW_EPI_RESID) {
+    // the next LayerNorm's statistics: lane m < M sums row m of the tile (fixed order) and adds the
+    // fixed-point pair into group cb % G (one atomic instruction pair per wave)
+    if (p.stats_out && lane < M && lane < 32) {
+      float s = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCB * 16; ++j) {
+        const float x = tile[lane][j];
+        s += x;
+        s2 += x * x;
+      }
+      unsigned long long* st =
+          reinterpret_cast<unsigned long long*>(p.stats_out + (int64_t)lane * p.ld_stats + 2 * (cg % G));
+      atomicAdd(st, (unsigned long long)(long long)llrint((double)s * S1));
+      atomicAdd(st + 1, (unsigned long long)(long long)llrint((double)s2 * S2));
+    }
+  }
+}
+
+__global__ void pack_kernel(const bf16_t* __restrict__ W, int N, int K, bf16_t* __restrict__ out) {
+  const int nkt = K >> 5;
+  const int64_t total = (int64_t)((N + 31) / 32 * 2) * nkt * 64;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int lane = (int)(i & 63);
+    const int64_t tile = i >> 6;
+    const int kt = (int)(tile % nkt);
+    const int cb = (int)(tile / nkt);
+    const int n = cb * 16 + (lane & 15);
+    const int k = kt * 32 + 8 * (lane >> 4);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < N) v = *reinterpret_cast<const uint4*>(W + (int64_t)n * K + k);
+    reinterpret_cast<uint4*>(out)[i] = v;
+  }
+}
+
+// Launch geometry for (N, K): column blocks per workgroup, k-tiles per wave, waves, K splits.
+struct Geo {
+  int ncb, ktm, nw, ks;
+};
+
+Geo choose(int64_t N, int64_t K) {
+  const int nkt = (int)(K / 32);
+  const int blocks = (int)((N + 15) / 16);
+  Geo g;
+  g.ncb = blocks >= 320 ? 2 : 1;  // wide matrices: reuse each activation fragment twice
+  g.ks = 1;
+  if (blocks < 128 && nkt > 80) g.ks = (nkt + 19) / 20;  // few columns, long K: split over workgroups
+  const int per_wg = (nkt + g.ks - 1) / g.ks;
+  g.ktm = (g.ncb == 1 && blocks >= 160 && per_wg <= 40) ? 5 : 10;
+  g.nw = (per_wg + g.ktm - 1) / g.ktm;
+  if (g.nw > MAXW) {  // very long K: more splits
+    g.nw = MAXW;
+    g.ks = (nkt + MAXW * g.ktm - 1) / (MAXW * g.ktm);
+  }
+  if (g.nw < 1) g.nw = 1;
+  return g;
+}
+
+template <int KTM, int NCB, bool LNA>
+hipError_t launch_store(const DecP& p, const Geo& g, bool c_f32, hipStream_t s) {
+  const dim3 grid((unsigned)((p.N + 16 * NCB - 1) / (16 * NCB)), (unsigned)g.ks);
+  const dim3 block((unsigned)(64 * g.nw));
+  if (c_f32)
+    hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, KW_EPI_STORE, float>), grid, block, 0, s, p, g.ks);
+  else
+    hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, KW_EPI_STORE, bf16_t>), grid, block, 0, s, p, g.ks);
+  return hipGetLastError();
+}
+
+template <int KTM, int NCB>
+hipError_t launch_k(const DecP& p, const Geo& g, bool c_f32, hipStream_t s) {
+  const dim3 grid((unsigned)((p.N + 16 * NCB - 1) / (16 * NCB)), (unsigned)g.ks);
+  const dim3 block((unsigned)(64 * g.nw));
+  if (p.epi == KW_EPI_RESID) {
+    if (p.ln_stats)
+      hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, true, KW_EPI_RESID, float>), grid, block, 0, s, p, g.ks);
+    else
+      hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, false, KW_EPI_RESID, float>), grid, block, 0, s, p, g.ks);
+    return hipGetLastError();
+  }
+  return p.ln_stats ? launch_store<KTM, NCB, true>(p, g, c_f32, s) : launch_store<KTM, NCB, false>(p, g, c_f32, s);
+}
+
+hipError_t launch(const DecP& p, const Geo& g, bool c_f32, hipStream_t s) {
+  if (g.ktm == 5) return g.ncb == 2 ? launch_k<5, 2>(p, g, c_f32, s) : launch_k<5, 1>(p, g, c_f32, s);
+  return g.ncb == 2 ? launch_k<10, 2>(p, g, c_f32, s) : launch_k<10, 1>(p, g, c_f32, s);
+}
+
+}  // namespace
+
+extern "C" size_t kw_dec_linear_workspace_bytes(int64_t N, int64_t K) {
+  const Geo g = choose(N, K);
+  const int64_t ncg = (N + 16 * g.ncb - 1) / (16 * g.ncb);
+  return (size_t)CNT_MAX * sizeof(int) + (g.ks > 1 ? (size_t)ncg * g.ks * g.ncb * 512 * sizeof(float) : 0);
+}
+
+extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
+  if (!a || !a->x || !a->W || a->M < 0 || a->N <= 0 || a->K <= 0 || a->K % 32 != 0 || a->ldx % 8 != 0 || a->ldx < a->K)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: null pointer or bad sizes (K % 32 == 0, ldx % 8 == 0)");
+  if (a->epilogue == KW_EPI_RESID) {
+    if (!a->h || !a->hb || a->ldh < a->N)
+      return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: RESID needs h (f32) and hb (bf16) with ldh >= N");
+  } else if (a->epilogue == KW_EPI_STORE) {
+    if (!a->C || a->ldc < a->N || (a->c_dtype != KW_DT_F32 && a->c_dtype != KW_DT_BF16))
+      return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: STORE needs C (f32 or bf16) with ldc >= N");
+  } else {
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: epilogue must be STORE or RESID");
+  }
+  if (a->ln_stats && (a->ld_stats < 2 * KW_LN_GROUPS || !a->ln_colsum))
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: fused LayerNorm needs ln_colsum and ld_stats >= 2 * KW_LN_GROUPS");
+  if (a->stats_out && (a->epilogue != KW_EPI_RESID || a->ld_stats < 2 * KW_LN_GROUPS))
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: stats_out needs the RESID epilogue and ld_stats >= 2 * KW_LN_GROUPS");
+  if (a->M == 0) return KW_OK;
+  const Geo g = choose(a->N, a->K);
+  const int nkt = (int)(a->K / 32);
+  if ((nkt + g.ks * g.nw - 1) / (g.ks * g.nw) > g.ktm || g.ks > KSMAX)
+    return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_linear: K too long for the k-tile budget");
+  const int64_t ncg = (a->N + 16 * g.ncb - 1) / (16 * g.ncb);
+  if (g.ks > 1) {
+    if (ncg > CNT_MAX) return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: split-K needs N <= 65536");
+    if (!a->workspace || a->ws_bytes < kw_dec_linear_workspace_bytes(a->N, a->K))
+      return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: needs a zero-filled workspace of kw_dec_linear_workspace_bytes()");
+  }
+  hipStream_t s = (hipStream_t)stream;
+  for (int64_t m0 = 0; m0 < a->M; m0 += 32) {  // 32-row chunks (weights re-streamed per chunk)
+    DecP p;
+    p.M = (int)(a->M - m0 < 32 ? a->M - m0 : 32);
+    p.N = (int)a->N;
+    p.K = (int)a->K;
+    p.x = reinterpret_cast<const bf16_t*>(a->x) + m0 * a->ldx;
+    p.ldx = a->ldx;
+    p.ld_stats = a->ld_stats;
+    p.ln_stats = a->ln_stats ? a->ln_stats + m0 * a->ld_stats : nullptr;
+    p.ln_eps = a->ln_eps;
+    p.ln_colsum = a->ln_colsum;
+    p.W = reinterpret_cast<const bf16x8*>(a->W);
+    p.bias = a->bias;
+    p.epi = a->epilogue;
+    const size_t csz = a->c_dtype == KW_DT_F32 ? 4 : 2;
+    p.C = a->C ? reinterpret_cast<char*>(a->C) + m0 * a->ldc * csz : nullptr;
+    p.ldc = a->ldc;
+    p.gelu = a->gelu;
+    p.scale = a->scale;
+    p.scale_cols = (int)a->scale_cols;
+    p.h = a->h ? a->h + m0 * a->ldh : nullptr;
+    p.hb = a->hb ? reinterpret_cast<bf16_t*>(a->hb) + m0 * a->ldh : nullptr;
+    p.ldh = a->ldh;
+    p.stats_out = a->stats_out ? a->stats_out + m0 * a->ld_stats : nullptr;
+    p.cnt = reinterpret_cast<int*>(a->workspace);
+    p.slab = a->workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(a->workspace) + CNT_MAX * sizeof(int)) : nullptr;
+    hipError_t e = launch(p, g, a->c_dtype == KW_DT_F32, s);
+    if (e != hipSuccess) return kw_set_error(e);
+  }
+  return KW_OK;
+}
+
+extern "C" size_t kw_packed_weight_bytes(int64_t N, int64_t K) { return (size_t)((N + 31) / 32) * 32 * (size_t)K * 2; }
+
+extern "C" int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed, kw_stream_t stream) {
+  if (!W || !packed || N <= 0 || K <= 0 || K % 32 != 0)
+    return kw_set_error_msg(KW_EINVAL, "kw_pack_weight: needs K % 32 == 0");
+  hipLaunchKernelGGL(pack_kernel, dim3(1024), dim3(256), 0, (hipStream_t)stream, (const bf16_t*)W, (int)N, (int)K,
+                     (bf16_t*)packed);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}

@@ -8,9 +8,8 @@
 //    time-major padded layout makes each im2col row a contiguous slice) and cross-K/V projection.
 //  * gemm_f32_kernel: exact-f32 path (v_mfma_f32_32x32x2_f32 = bitwise fmaf chain) used by the
 //    fp32 parity mode.
-//  * gemv_packed_kernel: decode-step skinny GEMM (M <= 128).  Weights pre-packed into 1-KB
-//    16x32 fragments so each wave streams W with perfectly coalesced 16-B/lane loads; activations
-//    come from L2; 4 waves split K and reduce through LDS.  HBM-bound (weights read once per step).
+//  * gemm256_kernel: 256x256x64 ping-pong for the large encoder GEMMs (see its header below).
+//  (decode-step skinny linears: declin.hip)
 // Shared epilogues: bias, exact GELU, column scale (q * head_dim^-0.5, modeling_whisper.py:309),
 // row-periodic add (encoder positions, :621-624), residual add into the f32 stream, head-split store.
 #include <stdlib.h>

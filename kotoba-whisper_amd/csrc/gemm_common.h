@@ -1,4 +1,4 @@
-// Shared GEMM parameter block and epilogue (gemm.hip, gemv.hip).
+// Shared GEMM parameter block and epilogue (gemm.hip).
 #pragma once
 #include "kw_common.h"
 
@@ -18,14 +18,6 @@ struct GemmP {
   const float* row_add;
   int row_add_period;
   int hs_seq, hs_heads, hs_hd;
-  // kw_gemv fused LayerNorm prologue / statistics epilogue
-  const float* ln_h;
-  const float* ln_stats;
-  int ln_slots;
-  float ln_eps;
-  float* stats_out;
-  void* ws;
-  size_t ws_bytes;
 };
 
 __device__ __forceinline__ int64_t row_off(int64_t r, int64_t rpb, int64_t bs, int64_t ld) {
@@ -72,9 +64,6 @@ inline GemmP to_params(const kw_gemm_args* a) {
   p.row_add = a->row_add; p.row_add_period = a->row_add_period > 0 ? (int)a->row_add_period : 1;
   p.hs_seq = a->hs_seq > 0 ? (int)a->hs_seq : 1; p.hs_heads = a->hs_heads > 0 ? (int)a->hs_heads : 1;
   p.hs_hd = a->hs_head_dim > 0 ? (int)a->hs_head_dim : 1;
-  p.ln_h = a->ln_h; p.ln_stats = a->ln_stats; p.ln_slots = (int)a->ln_slots;
-  p.ln_eps = a->ln_eps; p.stats_out = a->stats_out;
-  p.ws = a->workspace; p.ws_bytes = a->ws_bytes;
   if (p.c_rpb <= 0) p.c_rpb = 1;
   if (p.a_rpb <= 0) p.a_rpb = 1;
   return p;

@@ -35,8 +35,20 @@ class GemmArgs(ctypes.Structure):
         ("scale", ctypes.c_float), ("scale_cols", c_i64),
         ("row_add", c_vp), ("row_add_period", c_i64),
         ("hs_seq", c_i64), ("hs_heads", c_i64), ("hs_head_dim", c_i64),
-        ("ln_h", c_vp), ("ln_stats", c_vp), ("ln_slots", c_i64),
-        ("ln_eps", ctypes.c_float), ("stats_out", c_vp),
+    ]
+
+
+KW_LN_GROUPS = 8
+
+
+class DecLinearArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_i64), ("ln_stats", c_vp), ("ld_stats", c_i64), ("ln_eps", ctypes.c_float),
+        ("ln_colsum", c_vp), ("W", c_vp), ("bias", c_vp), ("epilogue", ctypes.c_int),
+        ("C", c_vp), ("ldc", c_i64), ("c_dtype", ctypes.c_int),
+        ("gelu", ctypes.c_int), ("scale", ctypes.c_float), ("scale_cols", c_i64),
+        ("h", c_vp), ("hb", c_vp), ("ldh", c_i64), ("stats_out", c_vp),
+        ("M", c_i64), ("N", c_i64), ("K", c_i64),
         ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
     ]
 
@@ -60,13 +72,15 @@ EXPORTS = {
     "kw_log_mel": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp, c_vp, c_vp]),
     "kw_mel_to_time_major": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp]),
     "kw_gemm": (ctypes.c_int, [ctypes.POINTER(GemmArgs), c_vp]),
-    "kw_gemv": (ctypes.c_int, [ctypes.POINTER(GemmArgs), c_vp]),
+    "kw_dec_linear": (ctypes.c_int, [ctypes.POINTER(DecLinearArgs), c_vp]),
+    "kw_dec_linear_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
     "kw_pack_weight": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "kw_packed_weight_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
-    "kw_gemv_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64, c_i64]),
+    "kw_dec_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
+                                    c_vp, c_i64, c_vp, c_i64, c_vp]),
     "kw_layernorm": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp]),
     "kw_attention": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
+    "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
     "kw_self_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
                                          c_vp, c_vp]),
     "kw_cross_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,

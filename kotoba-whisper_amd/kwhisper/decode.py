@@ -5,8 +5,8 @@ A ``DecodeSession`` owns the static caches and step buffers of one batch:
   * self K/V static cache [L][B][H][448][64] (replaces DynamicLayer's torch.cat growth,
     TF/cache_utils.py:127-145);
   * ids [B][448] int64, cur_len, unfinished flags -- all on device, advanced by kw_greedy_step.
-The prefill (prompt of P tokens) runs eagerly; the single-token step (32 x 11 kernels + final LN +
-LM head + sampler) is captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed: the step
+The prefill (prompt of P tokens) runs eagerly; the single-token step (embedding + 32 x 8 kernels +
+LM head with the final LayerNorm fused + sampler) is captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed: the step
 reads its position from device memory, so one graph serves every step.  The host only polls the
 device unfinished-row count a few steps behind the GPU (no per-step sync).
 """
@@ -40,12 +40,12 @@ class DecodeSession:
         self.logits = torch.empty((B, s.vocab_size), device=dev, dtype=torch.float32)
         self._bufs = {}
         self._plans = {}
-        # split-K scratch shared by every skinny GEMM of a step (stream-ordered; zeroed once)
+        # split-K seam scratch shared by every decode linear of a step (stream-ordered; zeroed once)
         ws = 0
         if eng.packed:
             for n_, k_ in ((3 * d, d), (d, d), (s.decoder_ffn_dim, d), (d, s.decoder_ffn_dim), (s.vocab_size, d)):
-                ws = max(ws, ops.gemv_workspace_bytes(B, n_, k_))
-        self.gemv_ws = torch.zeros(((ws + 3) // 4,), device=dev, dtype=torch.float32) if ws else None
+                ws = max(ws, ops.dec_linear_workspace_bytes(n_, k_))
+        self.lin_ws = torch.zeros(((ws + 3) // 4,), device=dev, dtype=torch.float32) if ws else None
         self._graph = None
         self._graph_key = None
         if enc is not None:
@@ -69,36 +69,18 @@ class DecodeSession:
                 # cross-attention partials + arrival counters (must start zeroed; kernels leave them zeroed)
                 ws=torch.zeros((ops.cross_attn_workspace_bytes(self.B, q, self.eng.H, _HD, self.T) // 4 + 1,),
                                device=dev, dtype=torch.float32),
-                # per-row LayerNorm statistics: (sum, sum of squares) per 16-column slot of h
-                stats=torch.zeros((rows * ((d + 15) // 16) * 2,), device=dev, dtype=torch.float32),
             )
+            if self.eng.packed:
+                # bf16 mirror of the residual stream (the LayerNorm-fused linears' operand) and the
+                # fixed-point statistics of every decoder LayerNorm: [3L+1][rows][2*KW_LN_GROUPS] int64
+                self._bufs[q]["hb"] = torch.empty((rows, d), device=dev, dtype=torch.bfloat16)
+                self._bufs[q]["stats"] = torch.zeros((3 * s.decoder_layers + 1, rows, ops.ln_stats_row_words()),
+                                                     device=dev, dtype=torch.int64)
         return self._bufs[q]
 
-    def _gemm(self, A, W, C, M, N, K, ln=None, stats_out=None, **kw):
-        """Row-chunked skinny GEMM (kw_gemv handles M <= 128) or the f32 GEMM in parity mode.
-
-        ``ln`` = (h, stats, slots, eps): fused LayerNorm prologue (gamma/beta folded into W, bias at load);
-        ``stats_out``: statistics epilogue."""
-        eng = self.eng
-        if not eng.packed:
-            return [ops.GemmPlan(A, W, C, M, N, K, **kw)]
-        plans = []
-        lda = kw.pop("lda", K)
-        ldc = kw.pop("ldc", N)
-        a_off = kw.pop("a_offset", 0)
-        ncb = (N + 15) // 16
-        chunk = 128  # kw_gemv limit (it launches 32-row chunks itself)
-        for m0 in range(0, M, chunk):
-            mm = min(chunk, M - m0)
-            lnc = None
-            if ln is not None:
-                h, st, slots, eps = ln
-                lnc = (h, st[m0 * slots * 2:], slots, eps)
-            so = stats_out[m0 * ncb * 2:] if stats_out is not None else None
-            plans.append(ops.GemmPlan(A, W, C, mm, N, K, lda=lda, ldc=ldc, a_offset=a_off + m0 * lda,
-                                      c_offset=m0 * ldc, packed=True, dtype=torch.bfloat16, ln=lnc, stats_out=so,
-                                      workspace=self.gemv_ws, **kw))
-        return plans
+    def _gemm(self, A, W, C, M, N, K, **kw):
+        """f32 parity-mode linear (kw_gemm)."""
+        return [ops.GemmPlan(A, W, C, M, N, K, **kw)]
 
     def _step_plans(self, q: int):
         """The decoder forward for q new positions per row (q = prompt length for the prefill, 1 after)."""
@@ -111,45 +93,52 @@ class DecodeSession:
         scale = _HD ** -0.5
         eps = s.layer_norm_eps
         if eng.packed:
-            # bf16 path: every decoder LayerNorm is fused into the GEMM that consumes it; its row statistics
-            # come from the embedding / residual-add epilogue that produced h.
-            st = b["stats"]
-            full = (d + 15) // 16
-            seq = [("embed", q, b["h"], st)]
-            slots = 1
+            # bf16 path: every decoder LayerNorm is fused into the linear that consumes it
+            # (operand = the bf16 residual mirror hb, statistics from the fixed-point accumulators its
+            # producer filled); the residual-add linears update h / hb and fill the next statistics.
+            st, hb, h = b["stats"], b["hb"], b["h"]
+            G2 = ops.ln_stats_row_words()
+            ws = self.lin_ws
+            lin = ops.DecLinearPlan
+            seq = [("dembed", q, h, hb, st[0], st[1:])]
             for li, lay in enumerate(eng.dec_layers):
-                seq += self._gemm(b["x"], lay["qkv_w"], b["qkv"], rows, 3 * d, d, bias=lay["qkv_b"], scale=scale,
-                                  scale_cols=d, ln=(b["h"], st, slots, eps))
+                k = 3 * li
+                seq.append(lin(hb, lay["qkv_w"], rows, 3 * d, d, ln=(st[k], 0, G2, eps, lay["qkv_cs"]), bias=lay["qkv_b"],
+                               C=b["qkv"], scale=scale, scale_cols=d, workspace=ws))
                 seq.append(("self", q, b["qkv"], li, b["attn"]))
-                seq += self._gemm(b["attn"], lay["o_w"], b["h"], rows, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID,
-                                  stats_out=st)
-                seq += self._gemm(b["x"], lay["xq_w"], b["qx"], rows, d, d, bias=lay["xq_b"], scale=scale, scale_cols=d,
-                                  ln=(b["h"], st, full, eps))
+                seq.append(lin(b["attn"], lay["o_w"], rows, d, d, bias=lay["o_b"], resid=(h, hb, d, 0),
+                               stats_out=(st[k + 1], 0, G2), workspace=ws))
+                seq.append(lin(hb, lay["xq_w"], rows, d, d, ln=(st[k + 1], 0, G2, eps, lay["xq_cs"]), bias=lay["xq_b"],
+                               C=b["qx"], scale=scale, scale_cols=d, workspace=ws))
                 seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
-                seq += self._gemm(b["attn"], lay["xo_w"], b["h"], rows, d, d, bias=lay["xo_b"], epilogue=L.KW_EPI_RESID,
-                                  stats_out=st)
-                seq += self._gemm(b["x"], lay["fc1_w"], b["ffn"], rows, s.decoder_ffn_dim, d, bias=lay["fc1_b"],
-                                  gelu=True, ln=(b["h"], st, full, eps))
-                seq += self._gemm(b["ffn"], lay["fc2_w"], b["h"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
-                                  epilogue=L.KW_EPI_RESID, stats_out=st)
-                slots = full
-        else:
-            seq = [("embed", q, b["h"], None)]
-            for li, lay in enumerate(eng.dec_layers):
-                seq.append(("ln", b["h"], lay["ln1_g"], lay["ln1_b"], b["x"]))
-                seq += self._gemm(b["x"], lay["qkv_w"], b["qkv"], rows, 3 * d, d, bias=lay["qkv_b"], scale=scale,
-                                  scale_cols=d)
-                seq.append(("self", q, b["qkv"], li, b["attn"]))
-                seq += self._gemm(b["attn"], lay["o_w"], b["h"], rows, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID)
-                seq.append(("ln", b["h"], lay["ln2_g"], lay["ln2_b"], b["x"]))
-                seq += self._gemm(b["x"], lay["xq_w"], b["qx"], rows, d, d, bias=lay["xq_b"], scale=scale, scale_cols=d)
-                seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
-                seq += self._gemm(b["attn"], lay["xo_w"], b["h"], rows, d, d, bias=lay["xo_b"], epilogue=L.KW_EPI_RESID)
-                seq.append(("ln", b["h"], lay["ln3_g"], lay["ln3_b"], b["x"]))
-                seq += self._gemm(b["x"], lay["fc1_w"], b["ffn"], rows, s.decoder_ffn_dim, d, bias=lay["fc1_b"],
-                                  gelu=True)
-                seq += self._gemm(b["ffn"], lay["fc2_w"], b["h"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
-                                  epilogue=L.KW_EPI_RESID)
+                seq.append(lin(b["attn"], lay["xo_w"], rows, d, d, bias=lay["xo_b"], resid=(h, hb, d, 0),
+                               stats_out=(st[k + 2], 0, G2), workspace=ws))
+                seq.append(lin(hb, lay["fc1_w"], rows, s.decoder_ffn_dim, d, ln=(st[k + 2], 0, G2, eps, lay["fc1_cs"]),
+                               bias=lay["fc1_b"], C=b["ffn"], gelu=True, workspace=ws))
+                seq.append(lin(b["ffn"], lay["fc2_w"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
+                               resid=(h, hb, d, 0), stats_out=(st[k + 3], 0, G2), workspace=ws))
+            # final LayerNorm (folded into the packed LM head) + proj_out on the last position of every row
+            Ld = s.decoder_layers
+            seq.append(lin(hb, eng.lm_w, B, s.vocab_size, d, ldx=q * d, x_offset=(q - 1) * d,
+                           ln=(st[3 * Ld], (q - 1) * G2, q * G2, eps, eng.lm_cs), bias=eng.lm_b, C=self.logits, workspace=ws))
+            self._plans[q] = seq
+            return seq
+        seq = [("embed", q, b["h"])]
+        for li, lay in enumerate(eng.dec_layers):
+            seq.append(("ln", b["h"], lay["ln1_g"], lay["ln1_b"], b["x"]))
+            seq += self._gemm(b["x"], lay["qkv_w"], b["qkv"], rows, 3 * d, d, bias=lay["qkv_b"], scale=scale,
+                              scale_cols=d)
+            seq.append(("self", q, b["qkv"], li, b["attn"]))
+            seq += self._gemm(b["attn"], lay["o_w"], b["h"], rows, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID)
+            seq.append(("ln", b["h"], lay["ln2_g"], lay["ln2_b"], b["x"]))
+            seq += self._gemm(b["x"], lay["xq_w"], b["qx"], rows, d, d, bias=lay["xq_b"], scale=scale, scale_cols=d)
+            seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
+            seq += self._gemm(b["attn"], lay["xo_w"], b["h"], rows, d, d, bias=lay["xo_b"], epilogue=L.KW_EPI_RESID)
+            seq.append(("ln", b["h"], lay["ln3_g"], lay["ln3_b"], b["x"]))
+            seq += self._gemm(b["x"], lay["fc1_w"], b["ffn"], rows, s.decoder_ffn_dim, d, bias=lay["fc1_b"],
+                              gelu=True)
+            seq += self._gemm(b["ffn"], lay["fc2_w"], b["h"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
+                              epilogue=L.KW_EPI_RESID)
         seq.append(("ln", b["h"], eng.dec_ln_g, eng.dec_ln_b, b["x"]))
         # LM head on the last position of every row (proj_out tied to embed_tokens, f32 logits)
         seq += self._gemm(b["x"], eng.lm_w, self.logits, B, s.vocab_size, d, lda=q * d, a_offset=(q - 1) * d)
@@ -167,7 +156,9 @@ class DecodeSession:
             if k == "ln":
                 ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4])
             elif k == "embed":
-                ops.embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2], p[3])
+                ops.embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2])
+            elif k == "dembed":
+                ops.dec_embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2], p[3], p[4], p[5])
             elif k == "self":
                 _, q, qkv, li, out = p
                 ops.self_attn_step(qkv, B, q, H, _HD, self.kc[li], self.vc[li], T_MAX, self.cur_len, out)

@@ -124,34 +124,35 @@ class WhisperEngine:
         self.dec_layers = []
         ckv_w, ckv_b = [], []
         def fold(w, b, ln):
-            """Packed (bf16) path: the LayerNorm feeding this projection is fused into kw_gemv, which forms
+            """Packed (bf16) path: the LayerNorm feeding this projection is fused into kw_dec_linear, which forms
             only (h - mean) * rstd; gamma/beta are folded here: W' = W diag(gamma), b' = b + W beta."""
             if not packed:
-                return pk(self._dev(w)), self._dev(b, f32)
+                return pk(self._dev(w)), self._dev(b, f32), None
             gam, bet = g(f"{ln}.weight").float(), g(f"{ln}.bias").float()
             w32 = w.float()
-            return pk(self._dev(w32 * gam[None, :])), self._dev(b.float() + w32 @ bet, f32)
+            wf = self._dev(w32 * gam[None, :])
+            return pk(wf), self._dev(b.float() + w32 @ bet, f32), ops.ln_colsum(wf)
 
         for i in range(s.decoder_layers):
             p = f"model.decoder.layers.{i}"
-            qkv_w, qkv_b = fold(*attn_qkv(f"{p}.self_attn"), f"{p}.self_attn_layer_norm")
-            xq_w, xq_b = fold(g(f"{p}.encoder_attn.q_proj.weight"), g(f"{p}.encoder_attn.q_proj.bias"),
-                              f"{p}.encoder_attn_layer_norm")
-            fc1_w, fc1_b = fold(g(f"{p}.fc1.weight"), g(f"{p}.fc1.bias"), f"{p}.final_layer_norm")
+            qkv_w, qkv_b, qkv_cs = fold(*attn_qkv(f"{p}.self_attn"), f"{p}.self_attn_layer_norm")
+            xq_w, xq_b, xq_cs = fold(g(f"{p}.encoder_attn.q_proj.weight"), g(f"{p}.encoder_attn.q_proj.bias"),
+                                     f"{p}.encoder_attn_layer_norm")
+            fc1_w, fc1_b, fc1_cs = fold(g(f"{p}.fc1.weight"), g(f"{p}.fc1.bias"), f"{p}.final_layer_norm")
             lay = dict(
                 ln1_g=self._dev(g(f"{p}.self_attn_layer_norm.weight"), f32),
                 ln1_b=self._dev(g(f"{p}.self_attn_layer_norm.bias"), f32),
-                qkv_w=qkv_w, qkv_b=qkv_b,
+                qkv_w=qkv_w, qkv_b=qkv_b, qkv_cs=qkv_cs,
                 o_w=pk(self._dev(g(f"{p}.self_attn.out_proj.weight"))),
                 o_b=self._dev(g(f"{p}.self_attn.out_proj.bias"), f32),
                 ln2_g=self._dev(g(f"{p}.encoder_attn_layer_norm.weight"), f32),
                 ln2_b=self._dev(g(f"{p}.encoder_attn_layer_norm.bias"), f32),
-                xq_w=xq_w, xq_b=xq_b,
+                xq_w=xq_w, xq_b=xq_b, xq_cs=xq_cs,
                 xo_w=pk(self._dev(g(f"{p}.encoder_attn.out_proj.weight"))),
                 xo_b=self._dev(g(f"{p}.encoder_attn.out_proj.bias"), f32),
                 ln3_g=self._dev(g(f"{p}.final_layer_norm.weight"), f32),
                 ln3_b=self._dev(g(f"{p}.final_layer_norm.bias"), f32),
-                fc1_w=fc1_w, fc1_b=fc1_b,
+                fc1_w=fc1_w, fc1_b=fc1_b, fc1_cs=fc1_cs,
                 fc2_w=pk(self._dev(g(f"{p}.fc2.weight"))), fc2_b=self._dev(g(f"{p}.fc2.bias"), f32),
             )
             self.dec_layers.append(lay)
@@ -161,7 +162,16 @@ class WhisperEngine:
         self.cross_kv_b = self._dev(torch.cat(ckv_b, 0), f32)
         self.dec_ln_g = self._dev(g("model.decoder.layer_norm.weight"), f32)
         self.dec_ln_b = self._dev(g("model.decoder.layer_norm.bias"), f32)
-        self.lm_w = pk(self.tok_emb) if packed else self.tok_emb
+        if packed:  # final LayerNorm folded into the packed LM head (kw_dec_linear forms only (x-mean)*rstd)
+            lg, lb = g("model.decoder.layer_norm.weight").float(), g("model.decoder.layer_norm.bias").float()
+            e32 = g("model.decoder.embed_tokens.weight").float()
+            lwf = self._dev(e32 * lg[None, :])
+            self.lm_w, self.lm_cs = pk(lwf), ops.ln_colsum(lwf)
+            self.lm_b = self._dev(e32 @ lb, f32)
+            del lwf
+            del e32
+        else:
+            self.lm_w, self.lm_b, self.lm_cs = self.tok_emb, None, None
         torch.cuda.synchronize(self.device)
 
     # ------------------------------------------------------------------------------------------

@@ -82,19 +82,16 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
 
 
 class GemmPlan:
-    """A pre-built ``kw_gemm`` / ``kw_gemv`` call: C = epilogue(A . W^T + bias)."""
+    """A pre-built ``kw_gemm`` call: C = epilogue(A . W^T + bias)."""
 
     def __init__(self, A, W, C, M, N, K, *, bias=None, lda=None, a_rows_per_batch=0, a_batch_stride=0,
                  ldc=None, c_rows_per_batch=0, c_batch_stride=0, epilogue=L.KW_EPI_STORE, gelu=False,
                  scale=1.0, scale_cols=0, row_add=None, row_add_period=0, hs_seq=0, hs_heads=0, hs_head_dim=0,
-                 packed=False, dtype=None, a_offset=0, c_offset=0, ln=None, stats_out=None, workspace=None):
-        """``ln`` = (h f32 [M][K], stats [M][slots][2], slots, eps): fused LayerNorm prologue
-        (kw_gemv only; A is then ignored; the LayerNorm's gamma/beta must be folded into W and bias).  ``stats_out``: row statistics epilogue (RESID only)."""
-        _cuda(A, W, C, bias, row_add, stats_out)
-        self._keep = (A, W, C, bias, row_add, ln, stats_out)
-        dt = _dt(W) if dtype is None else _DT[dtype]
+                 dtype=None, a_offset=0, c_offset=0):
+        _cuda(A, W, C, bias, row_add)
+        self._keep = (A, W, C, bias, row_add)
         a = L.GemmArgs()
-        a.dtype = dt
+        a.dtype = _dt(W) if dtype is None else _DT[dtype]
         a.c_dtype = _dt(C)
         a.A = A.data_ptr() + a_offset * A.element_size()
         a.lda = K if lda is None else lda
@@ -114,44 +111,113 @@ class GemmPlan:
         a.row_add = row_add.data_ptr() if row_add is not None else None
         a.row_add_period = row_add_period
         a.hs_seq, a.hs_heads, a.hs_head_dim = hs_seq, hs_heads, hs_head_dim
-        if ln is not None:
-            h, st, slots, eps = ln
-            _cuda(h, st)
-            a.ln_h = h.data_ptr() + a_offset * h.element_size()
-            a.ln_stats = st.data_ptr()
-            a.ln_slots = slots
-            a.ln_eps = float(eps)
-        if stats_out is not None:
-            a.stats_out = stats_out.data_ptr()
-        if packed:
-            need = gemv_workspace_bytes(M, N, K)
-            if workspace is None:
-                workspace = torch.zeros((need + 3) // 4, device=W.device, dtype=torch.float32)
-            if workspace.numel() * workspace.element_size() < need:
-                raise ValueError("gemv workspace too small")
-            a.workspace = workspace.data_ptr()
-            a.ws_bytes = workspace.numel() * workspace.element_size()
-            self._keep = self._keep + (workspace,)
         if bias is not None and bias.dtype != torch.float32:
             raise ValueError("bias must be float32")
         if row_add is not None and row_add.dtype != torch.float32:
             raise ValueError("row_add must be float32")
         self.args = a
-        self.packed = packed
-        self._fn = _lib().kw_gemv if packed else _lib().kw_gemm
-        self._name = "kw_gemv" if packed else "kw_gemm"
         self._ref = ctypes.byref(a)
 
     def __call__(self):
-        L.check(self._fn(self._ref, _s()), self._name)
+        L.check(_lib().kw_gemm(self._ref, _s()), "kw_gemm")
 
 
-def gemv_workspace_bytes(M: int, N: int, K: int) -> int:
-    return int(_lib().kw_gemv_workspace_bytes(M, N, K))
+def dec_linear_workspace_bytes(N: int, K: int) -> int:
+    return int(_lib().kw_dec_linear_workspace_bytes(N, K))
+
+
+def ln_stats_row_words() -> int:
+    """int64 words per row of a fixed-point LayerNorm statistics buffer (include/kwhisper.h)."""
+    return 2 * L.KW_LN_GROUPS
+
+
+class DecLinearPlan:
+    """A pre-built ``kw_dec_linear`` call (decode-step linear over packed weights).
+
+    ``x``: bf16 [M][ldx] activations (x_offset elements from the start); ``ln`` = (stats int64 tensor,
+    word offset, ld_stats, eps, colsum f32 [N]) fuses the LayerNorm of x (gamma/beta folded into W/bias
+    by the caller, colsum = row sums of the folded bf16 weight: ``ln_colsum``);
+    STORE writes ``C`` (f32 or bf16, ldc); RESID updates ``resid`` = (h f32, hb bf16 mirror, ldh, row
+    offset) and adds the next LayerNorm's statistics into ``stats_out`` = (tensor, word offset, ld_stats)."""
+
+    def __init__(self, x, W, M, N, K, *, ldx=None, x_offset=0, ln=None, bias=None, C=None, ldc=None, c_offset=0,
+                 gelu=False, scale=1.0, scale_cols=0, resid=None, stats_out=None, workspace=None):
+        _cuda(x, W, bias, C, workspace)
+        if x.dtype != torch.bfloat16 or W.dtype != torch.bfloat16:
+            raise ValueError("kw_dec_linear takes bf16 activations and packed bf16 weights")
+        if bias is not None and bias.dtype != torch.float32:
+            raise ValueError("bias must be float32")
+        a = L.DecLinearArgs()
+        keep = [x, W, bias, C, workspace]
+        a.x = x.data_ptr() + x_offset * 2
+        a.ldx = K if ldx is None else ldx
+        a.ld_stats = ln_stats_row_words()
+        if ln is not None:
+            st, off, ld, eps, colsum = ln
+            _cuda(st, colsum)
+            if st.dtype != torch.int64:
+                raise ValueError("LayerNorm statistics are int64 fixed point")
+            if colsum.dtype != torch.float32 or colsum.numel() < N:
+                raise ValueError("ln colsum must be float32 [N]")
+            a.ln_stats = st.data_ptr() + off * 8
+            a.ld_stats = ld
+            a.ln_eps = float(eps)
+            a.ln_colsum = colsum.data_ptr()
+            keep += [st, colsum]
+        a.W = W.data_ptr()
+        a.bias = bias.data_ptr() if bias is not None else None
+        if resid is not None:
+            h, hb, ldh, row0 = resid
+            _cuda(h, hb)
+            if h.dtype != torch.float32 or hb.dtype != torch.bfloat16:
+                raise ValueError("RESID needs an f32 residual and a bf16 mirror")
+            a.epilogue = L.KW_EPI_RESID
+            a.h = h.data_ptr() + row0 * ldh * 4
+            a.hb = hb.data_ptr() + row0 * ldh * 2
+            a.ldh = ldh
+            keep += [h, hb]
+            if stats_out is not None:
+                so, soff, sld = stats_out
+                _cuda(so)
+                if so.dtype != torch.int64:
+                    raise ValueError("LayerNorm statistics are int64 fixed point")
+                a.stats_out = so.data_ptr() + soff * 8
+                a.ld_stats = sld
+                keep.append(so)
+        else:
+            if C is None:
+                raise ValueError("STORE needs C")
+            a.epilogue = L.KW_EPI_STORE
+            a.C = C.data_ptr() + c_offset * C.element_size()
+            a.ldc = N if ldc is None else ldc
+            a.c_dtype = _dt(C)
+        a.gelu = int(bool(gelu))
+        a.scale = float(scale)
+        a.scale_cols = scale_cols
+        a.M, a.N, a.K = M, N, K
+        need = dec_linear_workspace_bytes(N, K)
+        if workspace is None:
+            workspace = torch.zeros((need + 3) // 4, device=W.device, dtype=torch.float32)
+            keep.append(workspace)
+        if workspace.numel() * workspace.element_size() < need:
+            raise ValueError("kw_dec_linear workspace too small")
+        a.workspace = workspace.data_ptr()
+        a.ws_bytes = workspace.numel() * workspace.element_size()
+        self._keep = tuple(keep)
+        self.args = a
+        self._ref = ctypes.byref(a)
+
+    def __call__(self):
+        L.check(_lib().kw_dec_linear(self._ref, _s()), "kw_dec_linear")
+
+
+def ln_colsum(W: torch.Tensor) -> torch.Tensor:
+    """f32 [N] row sums of a bf16 [N][K] weight (the values kw_dec_linear multiplies), accumulated in f64."""
+    return W.double().sum(1).float().contiguous()
 
 
 def pack_weight(W: torch.Tensor) -> torch.Tensor:
-    """[N][K] bf16 -> packed 16x32-fragment layout for kw_gemv."""
+    """[N][K] bf16 -> packed 16x32-fragment layout for kw_dec_linear."""
     _cuda(W)
     if W.dtype != torch.bfloat16 or W.dim() != 2 or not W.is_contiguous():
         raise ValueError("pack_weight expects a contiguous 2-D bfloat16 tensor")
@@ -170,10 +236,20 @@ def attention(qkv: torch.Tensor, B: int, H: int, T: int, hd: int, out: torch.Ten
     return out
 
 
-def embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h, stats_out=None):
-    _cuda(ids, cur_len, tok_emb, pos_emb, h, stats_out)
+def embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h):
+    _cuda(ids, cur_len, tok_emb, pos_emb, h)
     L.check(_lib().kw_embed(_dt(tok_emb), _p(ids), ids.stride(0), B, q_len, _p(cur_len), _p(tok_emb), _p(pos_emb),
-                            tok_emb.shape[1], _p(h), _p(stats_out), _s()), "kw_embed")
+                            tok_emb.shape[1], _p(h), _s()), "kw_embed")
+
+
+def dec_embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h, hb, stats, zero_stats=None):
+    """Embedding for the bf16 decode step: h, its bf16 mirror hb, the first LayerNorm's statistics
+    (``stats`` int64 [B*q_len][2*KW_LN_GROUPS]) and zeroing of the later accumulators ``zero_stats``."""
+    _cuda(ids, cur_len, tok_emb, pos_emb, h, hb, stats, zero_stats)
+    nz = zero_stats.numel() if zero_stats is not None else 0
+    L.check(_lib().kw_dec_embed(_dt(tok_emb), _p(ids), ids.stride(0), B, q_len, _p(cur_len), _p(tok_emb),
+                                _p(pos_emb), tok_emb.shape[1], _p(h), _p(hb), _p(stats), stats.stride(0),
+                                _p(zero_stats), nz, _s()), "kw_dec_embed")
 
 
 def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out):

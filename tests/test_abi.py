@@ -55,7 +55,8 @@ def _c_layout(struct, fields):
     return [int(x) for x in subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split()]
 
 
-@pytest.mark.parametrize("cname,pyname", [("kw_gemm_args", "GemmArgs"), ("kw_sampler_args", "SamplerArgs")])
+@pytest.mark.parametrize("cname,pyname", [("kw_gemm_args", "GemmArgs"), ("kw_sampler_args", "SamplerArgs"),
+                                          ("kw_dec_linear_args", "DecLinearArgs")])
 def test_struct_layout_matches_c(cname, pyname):
     from kwhisper import _lib
 

@@ -188,23 +188,37 @@ def test_gemm_f32_exactish(M, N, K):
     torch.testing.assert_close(C, ref, atol=2e-5, rtol=2e-5)
 
 
+S1, S2 = 2.0 ** 32, 2.0 ** 28  # fixed-point scales of the LayerNorm statistics (include/kwhisper.h)
+
+
+def _fixed_stats(h, groups=8):
+    """Reference fixed-point statistics of rows of h (group 0 holds the row; include/kwhisper.h)."""
+    hd = h.double()
+    st = torch.zeros(h.shape[0], groups, 2, dtype=torch.int64, device=h.device)
+    st[:, 0, 0] = torch.round(hd.sum(-1) * S1).long()
+    st[:, 0, 1] = torch.round((hd * hd).sum(-1) * S2).long()
+    return st.view(h.shape[0], 2 * groups)
+
+
 @pytest.mark.parametrize("M,N,K", [(1, 1280, 1280), (32, 3840, 1280), (32, 1280, 5120), (128, 5120, 1280),
-                                   (5, 51866, 1280), (32, 51865, 384)])
-def test_gemv_packed(M, N, K):
+                                   (5, 51866, 1280), (32, 51865, 384), (17, 1152, 384), (32, 384, 1536)])
+def test_dec_linear_store(M, N, K):
+    """Plain decode linear (bf16 x, packed W, f32 and bf16 C) against an fp32 reference of the same op."""
     A = torch.randn(M, K, device="cuda").bfloat16()
     W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
     b = torch.randn(N, device="cuda")
     Wp = ops.pack_weight(W)
     C = torch.empty(M, N, device="cuda")
-    ops.GemmPlan(A, Wp, C, M, N, K, bias=b, packed=True, dtype=torch.bfloat16)()
-    torch.testing.assert_close(C, _ref_gemm(A, W, b), atol=2e-3, rtol=2e-3)
-    H0 = torch.randn(M, N, device="cuda")
-    Hc = H0.clone()
-    ops.GemmPlan(A, Wp, Hc, M, N, K, bias=b, packed=True, epilogue=L.KW_EPI_RESID, dtype=torch.bfloat16)()
-    torch.testing.assert_close(Hc, H0 + _ref_gemm(A, W, b), atol=2e-3, rtol=2e-3)
+    ops.DecLinearPlan(A, Wp, M, N, K, bias=b, C=C)()
+    ref = _ref_gemm(A, W, b)
+    torch.testing.assert_close(C, ref, atol=2e-3, rtol=2e-3)
+    Cb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.DecLinearPlan(A, Wp, M, N, K, bias=b, C=Cb, gelu=True, scale=0.5, scale_cols=N // 3)()
+    r = torch.nn.functional.gelu(ref)
+    r[:, : N // 3] *= 0.5
+    torch.testing.assert_close(Cb.float(), r, atol=2e-2, rtol=1e-2)
 
 
-# ---------------------------------------------------------------- LayerNorm
 @pytest.mark.parametrize("rows,dim", [(1, 384), (48000, 1280), (33, 2048)])
 @pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
 def test_layernorm(rows, dim, out_dtype):
@@ -356,54 +370,66 @@ def test_greedy_step_vs_oracle(rt, n_hist):
     assert int(nun.item()) == int(unf.sum().item())
 
 
-@pytest.mark.parametrize("ksplit", [None, "4"])
 @pytest.mark.parametrize("M", [32, 5, 70])
-def test_gemv_fused_layernorm_and_stats(monkeypatch, ksplit, M):
-    """LayerNorm prologue from producer statistics (gamma/beta folded into W and bias, as the engine
-    loads them) + residual-statistics epilogue (decode fusion); with and without the K-split seam."""
-    if ksplit:
-        monkeypatch.setenv("KW_GEMV_KSPLIT", ksplit)
-    d, N = 1280, 3840
-    h = torch.randn(M, d, device="cuda") * 2 + 0.5
-    g = 1 + 0.1 * torch.randn(d, device="cuda")
-    bb = 0.1 * torch.randn(d, device="cuda")
-    # producer statistics with 80 slots of 16 columns
-    st = torch.stack([h.view(M, 80, 16).sum(-1), (h.view(M, 80, 16) ** 2).sum(-1)], -1).contiguous()
-    W = (torch.randn(N, d, device="cuda") / d ** 0.5).bfloat16()
+@pytest.mark.parametrize("N,K", [(3840, 1280), (1280, 5120)])
+def test_dec_linear_layernorm_resid_stats(M, N, K):
+    """LayerNorm-fused STORE (gamma/beta folded into W and bias, as the engine loads them) and the RESID
+    epilogue (h += ., bf16 mirror, fixed-point statistics of the next LayerNorm); K 5120 exercises the
+    K-split seam.  Statistics are integers: compared exactly against the same fixed-point sums up to the
+    f32 rounding of the 16-column partials."""
+    h = torch.randn(M, K, device="cuda") * 2 + 0.5
+    hb = h.bfloat16()
+    st = _fixed_stats(h)
+    g = 1 + 0.1 * torch.randn(K, device="cuda")
+    bb = 0.1 * torch.randn(K, device="cuda")
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
     bias = torch.randn(N, device="cuda")
-    Wp = ops.pack_weight((W.float() * g[None, :]).bfloat16())
+    Wf = (W.float() * g[None, :]).bfloat16()
+    Wp = ops.pack_weight(Wf)
     bias_f = bias + W.float() @ bb
     C = torch.empty(M, N, device="cuda")
-    dummy = torch.empty(M, d, device="cuda", dtype=torch.bfloat16)
-    ops.GemmPlan(dummy, Wp, C, M, N, d, bias=bias_f, packed=True, dtype=torch.bfloat16,
-                 ln=(h, st.view(-1), 80, 1e-5))()
-    xn = torch.nn.functional.layer_norm(h, (d,), g, bb, 1e-5).bfloat16()
-    torch.testing.assert_close(C, _ref_gemm(xn, W, bias), atol=3e-2, rtol=2e-2)
-    # statistics epilogue: h2 = h + A.W2^T + b2 ; stats of h2 per 16-col slot
-    W2 = (torch.randn(d, N, device="cuda") / N ** 0.5).bfloat16()
-    b2 = torch.randn(d, device="cuda")
+    ops.DecLinearPlan(hb, Wp, M, N, K, ln=(st, 0, 16, 1e-5, ops.ln_colsum(Wf)), bias=bias_f, C=C)()
+    mu = h.double().mean(-1, keepdim=True)
+    var = h.double().var(-1, unbiased=False, keepdim=True)
+    xn = ((hb.double() - mu) / torch.sqrt(var + 1e-5) * g.double() + bb.double()).float().bfloat16()
+    torch.testing.assert_close(C, _ref_gemm(xn, W, bias), atol=4e-2, rtol=2e-2)
+    # RESID: h2 = h0 + A.W2^T + b2 (N2 = K columns), hb mirror, statistics accumulated into zeroed groups
+    N2 = K
+    W2 = (torch.randn(N2, N, device="cuda") / N ** 0.5).bfloat16()
+    b2 = torch.randn(N2, device="cuda")
     A2 = torch.randn(M, N, device="cuda").bfloat16()
-    h2 = h.clone()
-    so = torch.zeros(M * 80 * 2, device="cuda")
-    ops.GemmPlan(A2, ops.pack_weight(W2), h2, M, d, N, bias=b2, packed=True, dtype=torch.bfloat16,
-                 epilogue=L.KW_EPI_RESID, stats_out=so)()
-    ref = h + _ref_gemm(A2, W2, b2)
+    h0 = torch.randn(M, N2, device="cuda")
+    h2, hb2 = h0.clone(), torch.empty(M, N2, device="cuda", dtype=torch.bfloat16)
+    so = torch.zeros(M, 16, dtype=torch.int64, device="cuda")
+    ops.DecLinearPlan(A2, ops.pack_weight(W2), M, N2, N, bias=b2, resid=(h2, hb2, N2, 0), stats_out=(so, 0, 16))()
+    ref = h0 + _ref_gemm(A2, W2, b2)
     torch.testing.assert_close(h2, ref, atol=2e-3, rtol=2e-3)
-    so = so.view(M, 80, 2)
-    torch.testing.assert_close(so[..., 0], h2.view(M, 80, 16).sum(-1), atol=1e-3, rtol=1e-4)
-    torch.testing.assert_close(so[..., 1], (h2.view(M, 80, 16) ** 2).sum(-1), atol=1e-2, rtol=1e-4)
+    assert torch.equal(hb2, h2.bfloat16())
+    s1 = so.view(M, 8, 2)[..., 0].sum(-1).double() / S1
+    s2 = so.view(M, 8, 2)[..., 1].sum(-1).double() / S2
+    torch.testing.assert_close(s1, h2.double().sum(-1), atol=1e-3, rtol=1e-6)
+    torch.testing.assert_close(s2, (h2.double() ** 2).sum(-1), atol=1e-2, rtol=1e-6)
+    # determinism: a second run accumulates bitwise the same integers
+    so2 = torch.zeros_like(so)
+    h3 = h0.clone()
+    ops.DecLinearPlan(A2, ops.pack_weight(W2), M, N2, N, bias=b2, resid=(h3, hb2, N2, 0), stats_out=(so2, 0, 16))()
+    assert torch.equal(so, so2) and torch.equal(h2, h3)
 
 
-def test_embed_stats():
+def test_dec_embed():
     B, q, d, V = 3, 2, 384, 1000
     tok = torch.randn(V, d, device="cuda").bfloat16()
     pos = torch.randn(448, d, device="cuda").bfloat16()
     ids = torch.randint(0, V, (B, 449), device="cuda")
     cur = torch.tensor([7], dtype=torch.int32, device="cuda")
     h = torch.empty(B * q, d, device="cuda")
-    st = torch.empty(B * q * 2, device="cuda")
-    ops.embed(ids, B, q, cur, tok, pos, h, st)
+    hb = torch.empty(B * q, d, device="cuda", dtype=torch.bfloat16)
+    st = torch.full((B * q, 16), 77, dtype=torch.int64, device="cuda")
+    later = torch.full((5, B * q, 16), 99, dtype=torch.int64, device="cuda")
+    ops.dec_embed(ids, B, q, cur, tok, pos, h, hb, st, later)
     ref = (tok[ids[:, 5:7]].float() + pos[5:7].float()).reshape(B * q, d)
     torch.testing.assert_close(h, ref)
-    torch.testing.assert_close(st.view(-1, 2)[:, 0], ref.sum(-1), atol=1e-3, rtol=1e-5)
-    torch.testing.assert_close(st.view(-1, 2)[:, 1], (ref ** 2).sum(-1), atol=1e-2, rtol=1e-5)
+    assert torch.equal(hb, ref.bfloat16())
+    assert torch.all(later == 0) and torch.all(st[:, 2:] == 0)
+    torch.testing.assert_close(st[:, 0].double() / S1, ref.double().sum(-1), atol=1e-3, rtol=1e-6)
+    torch.testing.assert_close(st[:, 1].double() / S2, (ref.double() ** 2).sum(-1), atol=1e-2, rtol=1e-6)

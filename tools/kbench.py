@@ -18,7 +18,6 @@ sys.path.insert(0, os.path.join(ROOT, "kotoba-whisper_amd"))
 
 import torch  # noqa: E402
 
-from kwhisper import _lib as L  # noqa: E402
 from kwhisper import ops  # noqa: E402
 
 
@@ -70,35 +69,40 @@ def main():
     dev = torch.device("cuda")
     B, d, H, S, F = 32, 1280, 20, 1500, 5120
     nl = a.layers
-    res = {"variant": os.environ.get("KW_GEMV_VARIANT", "0")}
+    res = {}
+    G2 = ops.ln_stats_row_words()
+    hb = torch.randn(B, F, device=dev).bfloat16()
     h = torch.randn(B, d, device=dev)
-    st = torch.stack([h.view(B, 80, 16).sum(-1), (h.view(B, 80, 16) ** 2).sum(-1)], -1).contiguous().view(-1)
-    g = torch.ones(d, device=dev)
-    bb = torch.zeros(d, device=dev)
-    x = torch.randn(B, F, device=dev).bfloat16()
+    st = torch.zeros(B, G2, dtype=torch.int64, device=dev)
+    st[:, 0] = (h.double().sum(-1) * 2 ** 32).long()
+    st[:, 1] = ((h.double() ** 2).sum(-1) * 2 ** 28).long()
+    ws = torch.zeros(1 << 22, device=dev)
     for name, N, K, lna, resid in [("qkv_ln", 3 * d, d, True, False), ("o_resid", d, d, False, True),
                                    ("xq_ln", d, d, True, False), ("fc1_ln_gelu", F, d, True, False),
                                    ("fc2_resid", d, F, False, True), ("o_plain", d, d, False, False),
-                                   ("lm_head", 51866, d, False, False)]:
+                                   ("lm_head", 51866, d, True, False)]:
         if not want(name):
             continue
         n_bufs = 1 if name == "lm_head" else nl
         Ws = [ops.pack_weight((torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()) for _ in range(n_bufs)]
+        cs = torch.zeros(N, device=dev)
         bias = torch.zeros(N, device=dev)
-        C = torch.empty(B, N, device=dev) if (resid or name == "lm_head") else torch.empty(B, N, device=dev,
-                                                                                          dtype=torch.bfloat16)
-        so = torch.zeros(B * ((N + 15) // 16) * 2, device=dev) if resid else None
+        C = torch.empty(B, N, device=dev) if name == "lm_head" else torch.empty(B, N, device=dev, dtype=torch.bfloat16)
+        hr = torch.zeros(B, N, device=dev)
+        hbr = torch.empty(B, N, device=dev, dtype=torch.bfloat16)
+        so = torch.zeros(B, G2, dtype=torch.int64, device=dev)
         plans = []
         for W in Ws:
-            kw = dict(bias=bias, packed=True, dtype=torch.bfloat16)
+            kw = dict(bias=bias, workspace=ws, ldx=F)
             if lna:
-                kw["ln"] = (h, st, 80, 1e-5)
+                kw["ln"] = (st, 0, G2, 1e-5, cs)
             if resid:
-                kw.update(epilogue=L.KW_EPI_RESID, stats_out=so)
+                kw.update(resid=(hr, hbr, N, 0), stats_out=(so, 0, G2))
+            else:
+                kw["C"] = C
             if name.startswith("fc1"):
                 kw["gelu"] = True
-            plans.append(ops.GemmPlan(x[:, :K].contiguous() if not lna else x[:, :K].contiguous(), W, C, B, N, K,
-                                      **kw))
+            plans.append(ops.DecLinearPlan(hb, W, B, N, K, **kw))
         us = timeit(plans, a.reps)
         res[name] = {"us": round(us, 2), "GBps": round(N * K * 2 / us / 1e3, 1)}
     # attention kernels
