@@ -77,31 +77,26 @@ typedef struct {
 
 int kw_gemm(const kw_gemm_args* args, kw_stream_t stream);
 
-/* ---- decode step (bf16 engine) ---------------------------------------------------------------
- * Fixed-point LayerNorm statistics: a row's statistics are KW_LN_GROUPS pairs of int64
- * (sum * 2^32, sum of squares * 2^28), added by independent producers (integer adds: the result is
- * bitwise independent of their order); mean = sum(pairs.sum) / 2^32 / K, var = sum(pairs.sq) / 2^28 / K
- * - mean^2.  Row pitch ld_stats (int64 elements, >= 2 * KW_LN_GROUPS). */
-#define KW_LN_GROUPS 8
+/* ---- decode step (bf16 engine) --------------------------------------------------------------- */
 
 /* Decode-step linear over packed weights, any M (launched in 32-row chunks):
- *   A = x (bf16 [M][ldx]) or, if ln_stats != NULL, the LayerNorm (x - mean) * rstd (eps ln_eps) of it,
+ *   A = x (bf16 [M][ldx]) or, if ln != 0, the LayerNorm (x - mean) * rstd (eps ln_eps) of each row of it,
  *   with gamma/beta folded into W / bias by the caller (W' = W diag(gamma), b' = b + W beta) and
- *   ln_colsum[n] = sum_k W'[n][k] (f32, of the bf16 values packed): computed as
- *   rstd * (x W'^T - mean * ln_colsum)
+ *   ln_colsum[n] = sum_k W'[n][k] (f32, of the bf16 values packed); computed as
+ *   rstd * (x W'^T - mean * ln_colsum) with each row's statistics taken from x itself
  *   (TF modeling_whisper.py:446,476,500 + 469-503, proj_out :1080);
  *   STORE: C[m][n] = act(acc + bias) * (n < scale_cols ? scale : 1), C f32 or bf16;
- *   RESID: h[m][n] += acc + bias (f32 residual, modeling_whisper.py:482,495,503), hb = bf16(h), and
- *          optionally the next LayerNorm's fixed-point statistics added into stats_out.
+ *   RESID: h[m][n] += acc + bias (f32 residual, modeling_whisper.py:482,495,503) and hb = bf16(h), the
+ *          bf16 mirror the next LayerNorm-fused linear reads.
  * W: packed by kw_pack_weight.  workspace: >= kw_dec_linear_workspace_bytes(N, K) bytes, zero-filled
- * before first use (calls leave it zeroed); one workspace may serve all calls on one stream. */
+ * before first use (calls leave it zeroed); one workspace may serve all calls on one stream.
+ * Results are bitwise deterministic (fixed-order reductions, no float atomics). */
 typedef struct {
   const void* x;
   int64_t ldx;
-  const int64_t* ln_stats;   /* [M][ld_stats] or NULL */
-  int64_t ld_stats;
+  int ln;                    /* fuse the LayerNorm of x (STORE only) */
   float ln_eps;
-  const float* ln_colsum;    /* [N], required with ln_stats */
+  const float* ln_colsum;    /* [N], required with ln */
   const void* W;
   const float* bias;         /* [N] f32 or NULL */
   int epilogue;              /* KW_EPI_STORE or KW_EPI_RESID */
@@ -114,7 +109,6 @@ typedef struct {
   float* h;                  /* RESID: f32 residual [M][ldh] (in/out) */
   void* hb;                  /* RESID: bf16 mirror [M][ldh] (out) */
   int64_t ldh;
-  int64_t* stats_out;        /* RESID: [M][ld_stats] accumulators of the next LayerNorm, or NULL */
   int64_t M, N, K;
   void* workspace;
   size_t ws_bytes;
@@ -125,14 +119,6 @@ size_t kw_dec_linear_workspace_bytes(int64_t N, int64_t K);
 /* W [N][K] bf16 -> packed [ceil(N/32)*2][K/32][64 lanes][8] bf16 (columns >= N zero); K % 32 == 0. */
 int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed, kw_stream_t stream);
 size_t kw_packed_weight_bytes(int64_t N, int64_t K);
-
-/* Decode-step embedding for the bf16 engine: as kw_embed, plus hb = bf16(h), the first LayerNorm's
- * statistics written to stats [B*q_len][ld_stats] (replacing, not adding), and n_zero int64 words
- * at zero_stats set to 0 (the accumulators the step's later RESID linears add into). */
-int kw_dec_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
-                 const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
-                 void* hb, int64_t* stats, int64_t ld_stats, int64_t* zero_stats, int64_t n_zero,
-                 kw_stream_t stream);
 
 /* LayerNorm (eps) over the last dim of x [rows][dim] f32 -> y [rows][dim] (y_dtype);
  * TF modeling_whisper.py:371,377,434,443,446,642,790. dim % 4 == 0, dim <= 2048. */
@@ -145,20 +131,24 @@ int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, int64_t T, in
                  kw_stream_t stream);
 
 /* Decoder input embedding: h[b*q_len+i] = tok_emb[ids[b][L-q_len+i]] + pos_emb[L-q_len+i]
- * with L = *cur_len read on device (TF modeling_whisper.py:737-762; no embed scale). */
+ * with L = *cur_len read on device (TF modeling_whisper.py:737-762; no embed scale); hb (optional,
+ * bf16, may be NULL) receives bf16(h) for the bf16 engine's LayerNorm-fused linears. */
 int kw_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
              const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
-             kw_stream_t stream);
+             void* hb, kw_stream_t stream);
 
 /* Decoder self-attention over a static cache (TF modeling_whisper.py:469-480, cache_utils.py:127-145):
  * appends k/v of the q_len newest positions [L-q_len, L) to k_cache/v_cache [B][H][t_max][hd],
- * then causal attention for those positions. qkv: [B*q_len][3*H*hd]; out [B*q_len][H*hd]. */
+ * then causal attention for those positions. qkv: [B*q_len][3*H*hd]; out [B*q_len][H*hd]; t_max <= 512.
+ * q_len == 1 needs workspace >= kw_self_attn_workspace(B, H, t_max) bytes, zero-filled before first use
+ * (arrival counters every call leaves at zero); q_len > 1 ignores it. */
 int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t q_len, int64_t H, int64_t hd,
                       void* k_cache, void* v_cache, int64_t t_max, const int32_t* cur_len, void* out,
-                      kw_stream_t stream);
+                      void* workspace, size_t ws_bytes, kw_stream_t stream);
+size_t kw_self_attn_workspace(int64_t B, int64_t H, int64_t t_max);
 
 /* Decoder cross-attention against cached encoder K/V [B][H][S][hd] (TF modeling_whisper.py:323-326).
- * q: [B*q_len][H*hd]; out: [B*q_len][H*hd]; workspace >= kw_cross_attn_workspace(...) bytes and
+ * q: [B*q_len][H*hd]; out: [B*q_len][H*hd]; S <= 2048; workspace >= kw_cross_attn_workspace(...) bytes and
  * ZERO-FILLED before its first use (it holds arrival counters that every call leaves at zero). */
 int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64_t H, int64_t hd,
                        const void* k, const void* v, int64_t S, void* out, void* workspace,

@@ -12,10 +12,13 @@
 //   (((row>>1)&1)<<2) for the transposed reads) -- both conflict-free.  O is normalised and staged
 //   through LDS for 16-B coalesced stores.
 // Encoder f32 path: exact-fp32 reference-order kernel for the parity mode.
-// Decoder self-attention (K10): static KV cache append + causal attention (q_len >= 1).
-// Decoder cross-attention (K11): split-S partial softmax over cached encoder K/V, 8 lanes per key row
-//   so every K and V load is a coalesced 1-KB wave access; the last-arriving split combines the
-//   partials in the same launch (arrival counter with agent-scope release/acquire).
+// Decoder self-attention (K10): static KV cache append + attention; one new position per row splits
+//   the keys into <= 256-key chunks like the cross-attention (prefill, q_len > 1: one workgroup per
+//   (b, h) walking the queries).
+// Decoder cross-attention (K11): split-S partial softmax over cached encoder K/V in <= 256-key chunks,
+//   8 lanes per key row so every K and V load is a coalesced 1-KB wave access, and every load of the
+//   chunk (64 KB) issued before the first score; the last-arriving chunk combines the partials in the
+//   same launch (write-through partials + arrival counter, MI355X_MICROARCH "Valid forms" row 1).
 #include <math.h>
 
 #include "kw_common.h"
@@ -339,6 +342,142 @@ __device__ __forceinline__ void attend_rows(const float qv[8], int k0, int k1, K
 }
 
 // ------------------------------------------------------------------------------------------------
+// Single-query attention over one chunk of <= 256 keys, every K and V load in flight at once
+// (256 threads = 32 key slots x 8 lanes; lane (slot, sub) holds 16 B of rows slot, slot+32, ...).
+// Returns the chunk's (m, l) to every thread and the unnormalised o[tid] to threads 0..63.
+// ------------------------------------------------------------------------------------------------
+template <typename T>
+struct Row8 {
+  uint4 u[sizeof(T) == 2 ? 1 : 2];
+};
+template <typename T>
+__device__ __forceinline__ Row8<T> ld_row8(const T* p) {
+  Row8<T> r;
+  r.u[0] = *reinterpret_cast<const uint4*>(p);
+  if constexpr (sizeof(T) == 4) r.u[1] = reinterpret_cast<const uint4*>(p)[1];
+  return r;
+}
+template <typename T>
+__device__ __forceinline__ void unpack8(const Row8<T>& r, float v[8]) {
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t w[4] = {r.u[0].x, r.u[0].y, r.u[0].z, r.u[0].w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  } else {
+    const uint32_t w[8] = {r.u[0].x, r.u[0].y, r.u[0].z, r.u[0].w, r.u[1].x, r.u[1].y, r.u[1].z, r.u[1].w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = __uint_as_float(w[i]);
+  }
+}
+
+template <typename T, typename KP, typename VP>
+__device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, KP kp, VP vp, float (*red)[64],
+                                             float* stat, float& m_out, float& l_out, float& o_out) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
+  Row8<T> kr[8], vr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) kr[j] = ld_row8<T>(kp(min(k0 + slot + 32 * j, k1 - 1)) + sub * 8);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) vr[j] = ld_row8<T>(vp(min(k0 + slot + 32 * j, k1 - 1)) + sub * 8);
+  float sc[8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float kv[8];
+    unpack8<T>(kr[j], kv);
+    float sj = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kv[i], sj);
+    sj += __shfl_xor(sj, 1, 64);
+    sj += __shfl_xor(sj, 2, 64);
+    sj += __shfl_xor(sj, 4, 64);
+    sc[j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
+    mx = fmaxf(mx, sc[j]);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) stat[wave] = mx;
+  __syncthreads();
+  const float m = fmaxf(fmaxf(stat[0], stat[1]), fmaxf(stat[2], stat[3]));
+  float lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[j] - m) : 0.f;
+    lsum += pj;
+    float vv[8];
+    unpack8<T>(vr[j], vv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
+  }
+  // lanes of one wave with equal sub hold the same dims: reduce over lane bits 3..5
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    acc[i] += __shfl_xor(acc[i], 8, 64);
+    acc[i] += __shfl_xor(acc[i], 16, 64);
+    acc[i] += __shfl_xor(acc[i], 32, 64);
+  }
+  lsum = wave_sum(lsum) * 0.125f;  // every row's p was counted by its 8 lanes (exact: power of two)
+  if (lane < 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
+  }
+  if (lane == 0) stat[4 + wave] = lsum;
+  __syncthreads();
+  m_out = m;
+  l_out = (stat[4] + stat[5]) + (stat[6] + stat[7]);
+  o_out = tid < HD ? (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]) : 0.f;
+}
+
+// Combine of per-chunk partials (m, l, o[64]) published write-through by each chunk's workgroup; the
+// last arriver (arrival counter) merges them in chunk order and writes the normalised output row.
+template <typename T>
+__device__ __forceinline__ void publish_and_combine(float* part, int* cnt, int ns, int split, float m, float l, float o,
+                                                    T* out_row, int* last_flag) {
+  const int tid = threadIdx.x;
+  float* w = part + (int64_t)split * (HD + 2);
+  if (tid < HD) __hip_atomic_store(w + 2 + tid, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) {
+    __hip_atomic_store(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(w + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const int prev = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *last_flag = prev == ns - 1;
+    if (prev == ns - 1) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!*last_flag || tid >= HD) return;
+  constexpr int NSMAX = 8;
+  float ms[NSMAX], ls[NSMAX], os[NSMAX];
+#pragma unroll
+  for (int q = 0; q < NSMAX; ++q) {
+    if (q < ns) {
+      ms[q] = __hip_atomic_load(part + q * (HD + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ls[q] = __hip_atomic_load(part + q * (HD + 2) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      os[q] = __hip_atomic_load(part + q * (HD + 2) + 2 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  float M = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < NSMAX; ++q)
+    if (q < ns) M = fmaxf(M, ms[q]);
+  float lt = 0.f, ot = 0.f;
+#pragma unroll
+  for (int q = 0; q < NSMAX; ++q)
+    if (q < ns) {
+      const float f = expf(ms[q] - M);
+      lt = fmaf(ls[q], f, lt);
+      ot = fmaf(os[q], f, ot);
+    }
+  TypeIO<T>::st(out_row + tid, ot / lt);
+}
+
+// ------------------------------------------------------------------------------------------------
 // decoder self-attention: append to the static cache, then causal attention (q_len >= 1).
 // New keys/values are read from the qkv rows themselves (never read back from the cache in the
 // same launch).
@@ -390,8 +529,7 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q
                                                          const T* __restrict__ kc, const T* __restrict__ vc, int S,
                                                          int chunk, float* __restrict__ ws, int* __restrict__ cnt,
                                                          T* __restrict__ out) {
-  __shared__ float sc[256];
-  __shared__ float red[32][65];
+  __shared__ float red[4][64];
   __shared__ float stat[8];
   __shared__ int last;
   const int row = blockIdx.x;  // (b*q_len + qi)*H + h
@@ -400,8 +538,7 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q
   const int h = row % H;
   const int bq = row / H;
   const int b = bq / q_len;
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int sub = lane & 7;
+  const int sub = threadIdx.x & 7;
   const int k0 = split * chunk;
   const int k1 = min(S, k0 + chunk);
   const T* kb = kc + ((int64_t)b * H + h) * S * HD;
@@ -409,43 +546,58 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q
   float qv[8];
   load8<T>(q + (int64_t)bq * H * HD + h * HD + sub * 8, qv);
   float m, l, o;
-  attend_rows<T>(qv, k0, k1, [&](int k) { return kb + (int64_t)k * HD; }, [&](int k) { return vb + (int64_t)k * HD; },
-                 sc, red, stat, m, l, o);
-  // publish the partial with write-through (sc1) stores: no release fence needed; the arrival
-  // counter add follows every storing wave's vmcnt(0) and a workgroup barrier (MI355X_MICROARCH
-  // "Valid forms" row 1); the last arriver reads the partials with sc1 loads (no acquire fence).
-  float* w = ws + ((int64_t)row * ns + split) * (HD + 2);
-  if (tid < HD) __hip_atomic_store(w + 2 + tid, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (tid == 0) {
-    __hip_atomic_store(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(w + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  attend_chunk<T>(qv, k0, k1, [&](int k) { return kb + (int64_t)k * HD; }, [&](int k) { return vb + (int64_t)k * HD; },
+                  red, stat, m, l, o);
+  T* orow = out + (int64_t)bq * H * HD + h * HD;
+  if (ns == 1) {
+    if (threadIdx.x < HD) TypeIO<T>::st(orow + threadIdx.x, o / l);
+    return;
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const int prev = __hip_atomic_fetch_add(cnt + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = (prev == ns - 1);
-    if (last) __hip_atomic_store(cnt + row, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  publish_and_combine<T>(ws + (int64_t)row * ns * (HD + 2), cnt + row, ns, split, m, l, o, orow, &last);
+}
+
+// decoder self-attention for one new position (q_len == 1): split 0 appends k/v at L-1; each split
+// attends over its <= 256-key chunk of [0, L) (the new row read from qkv, never from the cache in the
+// same launch); splits beyond L exit; the last arriving split combines.
+template <typename T>
+__global__ __launch_bounds__(256) void self_attn_step1(const T* __restrict__ qkv, int H, T* __restrict__ kc,
+                                                       T* __restrict__ vc, int t_max, const int32_t* __restrict__ cur_len,
+                                                       float* __restrict__ ws, int* __restrict__ cnt, T* __restrict__ out) {
+  __shared__ float red[4][64];
+  __shared__ float stat[8];
+  __shared__ int last;
+  const int bh = blockIdx.x, split = blockIdx.y;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const int tid = threadIdx.x, sub = tid & 7;
+  const int L = *cur_len;
+  const int d = H * HD;
+  const int p0 = L - 1;
+  const int k0 = split * 256;
+  if (k0 >= L) return;
+  const int ns = (L + 255) / 256;
+  T* kb = kc + ((int64_t)b * H + h) * t_max * HD;
+  T* vb = vc + ((int64_t)b * H + h) * t_max * HD;
+  const T* row = qkv + (int64_t)b * 3 * d + h * HD;
+  if (split == 0 && tid < 8) {
+    copy8<T>(kb + (int64_t)p0 * HD + tid * 8, row + d + tid * 8);
+    copy8<T>(vb + (int64_t)p0 * HD + tid * 8, row + 2 * d + tid * 8);
   }
-  __syncthreads();
-  if (!last) return;
-  if (tid < HD) {
-    const float* w0 = ws + (int64_t)row * ns * (HD + 2);
-    float M = -INFINITY;
-    for (int s2 = 0; s2 < ns; ++s2) M = fmaxf(M, __hip_atomic_load(w0 + s2 * (HD + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    float lt = 0.f, ot = 0.f;
-    for (int s2 = 0; s2 < ns; ++s2) {
-      const float ms = __hip_atomic_load(w0 + s2 * (HD + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float f = expf(ms - M);
-      lt = fmaf(__hip_atomic_load(w0 + s2 * (HD + 2) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), f, lt);
-      ot = fmaf(__hip_atomic_load(w0 + s2 * (HD + 2) + 2 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), f, ot);
-    }
-    TypeIO<T>::st(out + (int64_t)bq * H * HD + h * HD + tid, ot / lt);
+  float qv[8];
+  load8<T>(row + sub * 8, qv);
+  float m, l, o;
+  attend_chunk<T>(qv, k0, min(L, k0 + 256),
+                  [&](int k) -> const T* { return k < p0 ? kb + (int64_t)k * HD : row + d; },
+                  [&](int k) -> const T* { return k < p0 ? vb + (int64_t)k * HD : row + 2 * d; }, red, stat, m, l, o);
+  T* orow = out + (int64_t)b * d + h * HD;
+  if (ns == 1) {
+    if (tid < HD) TypeIO<T>::st(orow + tid, o / l);
+    return;
   }
+  publish_and_combine<T>(ws + (int64_t)bh * 2 * (HD + 2), cnt + bh, ns, split, m, l, o, orow, &last);
 }
 
 int cross_splits(int64_t S) {
-  int ns = (int)((S + 255) / 256);
+  int ns = (int)((S + 255) / 256);  // <= 256 keys per chunk (attend_chunk); <= 8 chunks (combine)
   if (ns < 1) ns = 1;
   return ns;
 }
@@ -472,19 +624,37 @@ extern "C" int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, in
   return KW_OK;
 }
 
+extern "C" size_t kw_self_attn_workspace(int64_t B, int64_t H, int64_t t_max) {
+  (void)t_max;  // t_max <= 512: at most two 256-key chunks per (b, h)
+  return (size_t)(B * H) * 2 * (HD + 2) * sizeof(float) + (size_t)(B * H) * sizeof(int);
+}
+
 extern "C" int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t q_len, int64_t H, int64_t hd,
                                  void* k_cache, void* v_cache, int64_t t_max, const int32_t* cur_len, void* out,
-                                 kw_stream_t stream) {
+                                 void* workspace, size_t ws_bytes, kw_stream_t stream) {
   if (!qkv || !k_cache || !v_cache || !cur_len || !out || B <= 0 || q_len <= 0 || H <= 0 || t_max <= 0 || t_max > 512)
     return kw_set_error_msg(KW_EINVAL, "kw_self_attn_step: invalid arguments (t_max <= 512)");
   if (hd != HD) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_self_attn_step: head_dim must be 64");
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == KW_DT_BF16)
+  if (q_len == 1) {
+    if (!workspace || ws_bytes < kw_self_attn_workspace(B, H, t_max))
+      return kw_set_error_msg(KW_EINVAL, "kw_self_attn_step: needs a zero-filled workspace of kw_self_attn_workspace()");
+    float* part = (float*)workspace;
+    int* cnt = (int*)((char*)workspace + (size_t)(B * H) * 2 * (HD + 2) * sizeof(float));
+    dim3 grid((unsigned)(B * H), (unsigned)((t_max + 255) / 256));
+    if (dtype == KW_DT_BF16)
+      hipLaunchKernelGGL(self_attn_step1<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)qkv, (int)H, (bf16_t*)k_cache,
+                         (bf16_t*)v_cache, (int)t_max, cur_len, part, cnt, (bf16_t*)out);
+    else
+      hipLaunchKernelGGL(self_attn_step1<float>, grid, dim3(256), 0, s, (const float*)qkv, (int)H, (float*)k_cache,
+                         (float*)v_cache, (int)t_max, cur_len, part, cnt, (float*)out);
+  } else if (dtype == KW_DT_BF16) {
     hipLaunchKernelGGL(self_attn_step<bf16_t>, dim3((unsigned)(B * H)), dim3(256), 0, s, (const bf16_t*)qkv, (int)q_len,
                        (int)H, (bf16_t*)k_cache, (bf16_t*)v_cache, (int)t_max, cur_len, (bf16_t*)out);
-  else
+  } else {
     hipLaunchKernelGGL(self_attn_step<float>, dim3((unsigned)(B * H)), dim3(256), 0, s, (const float*)qkv, (int)q_len,
                        (int)H, (float*)k_cache, (float*)v_cache, (int)t_max, cur_len, (float*)out);
+  }
   KW_CHECK_LAUNCH();
   return KW_OK;
 }
@@ -506,6 +676,7 @@ extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q
   if (hd != HD) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_cross_attn_step: head_dim must be 64");
   if (ws_bytes < kw_cross_attn_workspace(B, q_len, H, hd, S))
     return kw_set_error_msg(KW_EINVAL, "kw_cross_attn_step: workspace too small");
+  if (S > 2048) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_cross_attn_step: S <= 2048 (8 chunks of 256)");
   const int ns = cross_splits(S);
   const int chunk = (int)((S + ns - 1) / ns);
   hipStream_t s = (hipStream_t)stream;

@@ -13,37 +13,33 @@
 //    split K and reduce through LDS; for few-column matrices with long K (fc2: N 1280, K 5120) KS
 //    workgroups split K with a deterministic seam (write-through partial slabs, an arrival counter,
 //    the last arriver sums the KS slabs in fixed order -- MI355X_MICROARCH "Valid forms" row 1);
-//  * fused LayerNorm: LN(x) W'^T = rstd * (x W'^T - mean * colsum(W')), so the MFMAs take the bf16
-//    residual mirror x as it is and the LayerNorm costs one multiply-add per output in the epilogue,
-//    with (mean, rstd) from per-row fixed-point statistics; gamma/beta are folded into W and bias at
-//    load time (W' = W diag(gamma), b' = b + W beta) and colsum(W') is precomputed per column;
-//  * RESID epilogue: h(f32) += acc + bias, the bf16 mirror hb = h for the next LayerNorm's operand,
-//    and the next LayerNorm's row statistics: every finishing column block adds its rows' (sum,
-//    sum of squares) as FIXED-POINT int64 (scales 2^32 / 2^28) into one of KW_LN_GROUPS accumulators
-//    per row.  Integer addition is associative, so the statistics -- and the tokens -- are bitwise
-//    deterministic whatever the workgroup order.
+//  * fused LayerNorm: a LayerNorm consumer's workgroup holds its 32 rows of the bf16 residual mirror
+//    x whole (its waves split K), so it computes each row's sum and sum of squares itself on the
+//    matrix cores (X.1 and the diagonal of X.X^T, fixed-order fp32) and applies the LayerNorm
+//    algebraically,
+//    LN(x) W'^T = rstd * (x W'^T - mean * colsum(W')): the MFMAs take x as it is and the LayerNorm
+//    costs one multiply-add per output; gamma/beta are folded into W and bias at load time
+//    (W' = W diag(gamma), b' = b + W beta) and colsum(W') is precomputed per column;
+//  * RESID epilogue: h(f32) += acc + bias, plus the bf16 mirror hb = h (the next LayerNorm's operand).
+// Everything is bitwise deterministic: no float atomics, every reduction in a fixed order.
 #include <stdlib.h>
 
 #include "kw_common.h"
 
 namespace {
 
-constexpr int G = KW_LN_GROUPS;
-constexpr double S1 = 4294967296.0;  // 2^32: fixed-point scale of row sums
-constexpr double S2 = 268435456.0;   // 2^28: fixed-point scale of row sums of squares
-constexpr int CNT_MAX = 4096;        // seam arrival counters at the start of the workspace
-constexpr int MAXW = 8;              // waves per workgroup
+constexpr int CNT_MAX = 4096;  // seam arrival counters at the start of the workspace
+constexpr int MAXW = 8;        // waves per workgroup
+constexpr int KSMAX = 8;       // K splits per column group (host-checked)
 
 struct DecP {
   const bf16_t* x;
   int64_t ldx;
-  const int64_t* ln_stats;
-  int64_t ld_stats;
+  int ln;
   float ln_eps;
   const float* ln_colsum;
   const bf16x8* W;
   const float* bias;
-  int epi;
   void* C;
   int64_t ldc;
   int gelu;
@@ -52,19 +48,16 @@ struct DecP {
   float* h;
   bf16_t* hb;
   int64_t ldh;
-  int64_t* stats_out;
   int M, N, K;
   float* slab;
   int* cnt;
 };
 
-constexpr int KSMAX = 8;  // K splits per column group (host-checked)
-
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
 __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
   __shared__ f32x4 red[MAXW][NCB][2][64];
-  __shared__ float rstat[32][2];             // LayerNorm (mean, rstd) per row
-  __shared__ float tile[32][NCB * 16 + 1];   // RESID: the block's new h values, for row statistics
+  __shared__ float rpart[MAXW][32][2];  // LayerNorm: per-wave row (sum, sum of squares)
+  __shared__ float rstat[32][2];     // LayerNorm: (mean, rstd) per row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int cg = blockIdx.x, ks = blockIdx.y;
   const int nkt = p.K >> 5;
@@ -87,15 +80,6 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
     const int k = min(kt0 + u, ktl) * 32 + akoff;
     a0[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r0 * p.ldx + k);
     a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
-  }
-  // LayerNorm statistics of the 32 rows (last wave: its loads queue behind the fewest weight loads... all
-  // waves issue the same count; wave nw-1 is as good as any) -> rstat in LDS
-  const bool stat_wave = LNA && wave == nw - 1 && lane < 32;
-  longlong2 stv[G];
-  if (stat_wave) {
-    const longlong2* sp = reinterpret_cast<const longlong2*>(p.ln_stats + (int64_t)min(lane, M - 1) * p.ld_stats);
-#pragma unroll
-    for (int g = 0; g < G; ++g) stv[g] = sp[g];
   }
   // epilogue operands of wave 0 (lane <-> column lane&15, rows 4*(lane>>4)+r and 16+...)
   float hold[NCB][2][4];
@@ -132,21 +116,40 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
       }
     }
   }
-  if (stat_wave) {
-    int64_t sa = 0, sb = 0;
+
+  // 3. LayerNorm statistics of the 32 rows (the workgroup's waves cover K: host-checked, ksn == 1), on
+  //    the matrix cores: X.1 gives the row sums, X.X^T's diagonal the row sums of squares (the A
+  //    fragment of X is also the B fragment of X^T); fixed-order fp32 accumulation, waves summed in
+  //    order through LDS
+  if constexpr (LNA) {
+    bf16x8 ones;
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      sa += stv[g].x;
-      sb += stv[g].y;
+    for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+    f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0, q0 = s0, q1 = s0;
+#pragma unroll
+    for (int u = 0; u < KTM; ++u)
+      if (kt0 + u < kt1) {
+        s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], ones, s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], ones, s1, 0, 0, 0);
+        q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], a0[u], q0, 0, 0, 0);
+        q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], a1[u], q1, 0, 0, 0);
+      }
+    // C layout: lane holds rows 4*(lane>>4)+i, column lane&15
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        rpart[wave][4 * (lane >> 4) + i][0] = s0[i];
+        rpart[wave][16 + 4 * (lane >> 4) + i][0] = s1[i];
+      }
     }
-    const double inv = 1.0 / p.K;
-    const double mean = (double)sa * (inv / S1);
-    const double var = fmax((double)sb * (inv / S2) - mean * mean, 0.0);
-    rstat[lane][0] = (float)mean;
-    rstat[lane][1] = rsqrtf((float)var + p.ln_eps);
+    const int di = (lane & 15) - 4 * (lane >> 4);  // diagonal element of this lane, if any
+    if (di >= 0 && di < 4) {
+      rpart[wave][lane & 15][1] = q0[di];
+      rpart[wave][16 + (lane & 15)][1] = q1[di];
+    }
   }
 
-  // 3. reduce the waves' K slices (fixed order); wave 0 continues
+  // 4. reduce the waves' K slices (fixed order); wave 0 continues
   if (nw > 1) {
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
@@ -162,8 +165,21 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
         c1[c] += red[w2][c][1][lane];
       }
   }
+  if constexpr (LNA) {  // wave 0: lane r < 32 sums row r's wave partials in wave order -> (mean, rstd)
+    if (lane < 32) {
+      float sx = 0.f, sq = 0.f;
+      for (int w2 = 0; w2 < nw; ++w2) {
+        sx += rpart[w2][lane][0];
+        sq += rpart[w2][lane][1];
+      }
+      const float inv = 1.f / (float)p.K;
+      const float mean = sx * inv;
+      rstat[lane][0] = mean;
+      rstat[lane][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + p.ln_eps);
+    }
+  }
 
-  // 4. K-split seam: publish the partial tile write-through, count arrivals, the last one sums in order
+  // 5. K-split seam: publish the partial tile write-through, count arrivals, the last one sums in order
   if (ksn > 1) {
     float* mine = p.slab + ((int64_t)cg * ksn + ks) * (NCB * 512);
 #pragma unroll
@@ -209,7 +225,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
       }
   }
 
-  // 5. epilogue: MFMA C layout -> element (row 4*(lane>>4)+r [+16], column lane&15)
+  // 6. epilogue: MFMA C layout -> element (row 4*(lane>>4)+r [+16], column lane&15)
 #pragma unroll
   for (int c = 0; c < NCB; ++c) {
     const int cb = cg * NCB + c;
@@ -224,10 +240,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
         const int m = 16 * hh + 4 * (lane >> 4) + r;
         const bool valid = nvalid && m < M;
         float v = hh ? c1[c][r] : c0[c][r];
-        if constexpr (LNA) {  // LN(x) W'^T = rstd * (x W'^T - mean * colsum(W'))
-          const int mr = min(m, 31);
-          v = rstat[mr][1] * (v - rstat[mr][0] * cs);
-        }
+        if constexpr (LNA) v = rstat[m][1] * (v - rstat[m][0] * cs);  // LN(x) W'^T
         v += bn;
         if constexpr (EPI == KW_EPI_RESID) {
           v += hold[c][hh][r];
@@ -235,30 +248,12 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
             p.h[(int64_t)m * p.ldh + n] = v;
             p.hb[(int64_t)m * p.ldh + n] = f2bf(v);
           }
-          tile[m][c * 16 + (lane & 15)] = valid ? v : 0.f;
         } else {
           if (p.gelu) v = gelu_erf(v);
           if (n < p.scale_cols) v *= p.scale;
           if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
         }
       }
-    }
-  }
-  if constexpr (EPI == KW_EPI_RESID) {
-    // the next LayerNorm's statistics: lane m < M sums row m of the tile (fixed order) and adds the
-    // fixed-point pair into group cb % G (one atomic instruction pair per wave)
-    if (p.stats_out && lane < M && lane < 32) {
-      float s = 0.f, s2 = 0.f;
-#pragma unroll
-      for (int j = 0; j < NCB * 16; ++j) {
-        const float x = tile[lane][j];
-        s += x;
-        s2 += x * x;
-      }
-      unsigned long long* st =
-          reinterpret_cast<unsigned long long*>(p.stats_out + (int64_t)lane * p.ld_stats + 2 * (cg % G));
-      atomicAdd(st, (unsigned long long)(long long)llrint((double)s * S1));
-      atomicAdd(st + 1, (unsigned long long)(long long)llrint((double)s2 * S2));
     }
   }
 }
@@ -314,22 +309,19 @@ hipError_t launch_store(const DecP& p, const Geo& g, bool c_f32, hipStream_t s) 
 }
 
 template <int KTM, int NCB>
-hipError_t launch_k(const DecP& p, const Geo& g, bool c_f32, hipStream_t s) {
+hipError_t launch_k(const DecP& p, bool resid, const Geo& g, bool c_f32, hipStream_t s) {
   const dim3 grid((unsigned)((p.N + 16 * NCB - 1) / (16 * NCB)), (unsigned)g.ks);
   const dim3 block((unsigned)(64 * g.nw));
-  if (p.epi == KW_EPI_RESID) {
-    if (p.ln_stats)
-      hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, true, KW_EPI_RESID, float>), grid, block, 0, s, p, g.ks);
-    else
-      hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, false, KW_EPI_RESID, float>), grid, block, 0, s, p, g.ks);
+  if (resid) {  // (no LayerNorm-fused residual linear in the decoder)
+    hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, false, KW_EPI_RESID, float>), grid, block, 0, s, p, g.ks);
     return hipGetLastError();
   }
-  return p.ln_stats ? launch_store<KTM, NCB, true>(p, g, c_f32, s) : launch_store<KTM, NCB, false>(p, g, c_f32, s);
+  return p.ln ? launch_store<KTM, NCB, true>(p, g, c_f32, s) : launch_store<KTM, NCB, false>(p, g, c_f32, s);
 }
 
-hipError_t launch(const DecP& p, const Geo& g, bool c_f32, hipStream_t s) {
-  if (g.ktm == 5) return g.ncb == 2 ? launch_k<5, 2>(p, g, c_f32, s) : launch_k<5, 1>(p, g, c_f32, s);
-  return g.ncb == 2 ? launch_k<10, 2>(p, g, c_f32, s) : launch_k<10, 1>(p, g, c_f32, s);
+hipError_t launch(const DecP& p, bool resid, const Geo& g, bool c_f32, hipStream_t s) {
+  if (g.ktm == 5) return g.ncb == 2 ? launch_k<5, 2>(p, resid, g, c_f32, s) : launch_k<5, 1>(p, resid, g, c_f32, s);
+  return g.ncb == 2 ? launch_k<10, 2>(p, resid, g, c_f32, s) : launch_k<10, 1>(p, resid, g, c_f32, s);
 }
 
 }  // namespace
@@ -352,14 +344,12 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
   } else {
     return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: epilogue must be STORE or RESID");
   }
-  if (a->ln_stats && (a->ld_stats < 2 * KW_LN_GROUPS || !a->ln_colsum))
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: fused LayerNorm needs ln_colsum and ld_stats >= 2 * KW_LN_GROUPS");
-  if (a->stats_out && (a->epilogue != KW_EPI_RESID || a->ld_stats < 2 * KW_LN_GROUPS))
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: stats_out needs the RESID epilogue and ld_stats >= 2 * KW_LN_GROUPS");
+  if (a->ln && (!a->ln_colsum || a->epilogue != KW_EPI_STORE))
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: fused LayerNorm needs ln_colsum and the STORE epilogue");
   if (a->M == 0) return KW_OK;
   const Geo g = choose(a->N, a->K);
   const int nkt = (int)(a->K / 32);
-  if ((nkt + g.ks * g.nw - 1) / (g.ks * g.nw) > g.ktm || g.ks > KSMAX)
+  if ((nkt + g.ks * g.nw - 1) / (g.ks * g.nw) > g.ktm || g.ks > KSMAX || (a->ln && g.ks > 1))
     return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_linear: K too long for the k-tile budget");
   const int64_t ncg = (a->N + 16 * g.ncb - 1) / (16 * g.ncb);
   if (g.ks > 1) {
@@ -375,13 +365,11 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     p.K = (int)a->K;
     p.x = reinterpret_cast<const bf16_t*>(a->x) + m0 * a->ldx;
     p.ldx = a->ldx;
-    p.ld_stats = a->ld_stats;
-    p.ln_stats = a->ln_stats ? a->ln_stats + m0 * a->ld_stats : nullptr;
+    p.ln = a->ln;
     p.ln_eps = a->ln_eps;
     p.ln_colsum = a->ln_colsum;
     p.W = reinterpret_cast<const bf16x8*>(a->W);
     p.bias = a->bias;
-    p.epi = a->epilogue;
     const size_t csz = a->c_dtype == KW_DT_F32 ? 4 : 2;
     p.C = a->C ? reinterpret_cast<char*>(a->C) + m0 * a->ldc * csz : nullptr;
     p.ldc = a->ldc;
@@ -391,10 +379,9 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     p.h = a->h ? a->h + m0 * a->ldh : nullptr;
     p.hb = a->hb ? reinterpret_cast<bf16_t*>(a->hb) + m0 * a->ldh : nullptr;
     p.ldh = a->ldh;
-    p.stats_out = a->stats_out ? a->stats_out + m0 * a->ld_stats : nullptr;
     p.cnt = reinterpret_cast<int*>(a->workspace);
     p.slab = a->workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(a->workspace) + CNT_MAX * sizeof(int)) : nullptr;
-    hipError_t e = launch(p, g, a->c_dtype == KW_DT_F32, s);
+    hipError_t e = launch(p, a->epilogue == KW_EPI_RESID, g, a->c_dtype == KW_DT_F32, s);
     if (e != hipSuccess) return kw_set_error(e);
   }
   return KW_OK;

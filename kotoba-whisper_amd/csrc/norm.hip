@@ -88,53 +88,17 @@ __global__ __launch_bounds__(256) void mel_tm_kernel(const float* __restrict__ m
 template <typename TW>
 __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, int64_t ids_stride, int q_len,
                                                     const int32_t* __restrict__ cur_len, const TW* __restrict__ tok,
-                                                    const TW* __restrict__ pos, int d, float* __restrict__ h) {
+                                                    const TW* __restrict__ pos, int d, float* __restrict__ h,
+                                                    bf16_t* __restrict__ hb) {
   const int r = blockIdx.x;  // b*q_len + i
   const int b = r / q_len, i = r - b * q_len;
   const int p = *cur_len - q_len + i;
   const int64_t id = ids[(int64_t)b * ids_stride + p];
-  for (int c = threadIdx.x; c < d; c += blockDim.x)
-    h[(int64_t)r * d + c] = TypeIO<TW>::ld(tok + id * d + c) + TypeIO<TW>::ld(pos + (int64_t)p * d + c);
-}
-
-// ---- decode-step embedding for the bf16 engine (kw_dec_embed) ----------------------------------------
-// h = tok[id] + pos[p] (f32), hb = bf16(h), and the first LayerNorm's fixed-point row statistics
-// (group 0 holds the whole row, groups 1.. are zero); the workgroups also zero the statistics
-// accumulators of the step's later LayerNorms (zero_stats, n_zero int64 words).
-template <typename TW>
-__global__ __launch_bounds__(256) void dec_embed_kernel(const int64_t* __restrict__ ids, int64_t ids_stride, int q_len,
-                                                        const int32_t* __restrict__ cur_len, const TW* __restrict__ tok,
-                                                        const TW* __restrict__ pos, int d, float* __restrict__ h,
-                                                        bf16_t* __restrict__ hb, int64_t* __restrict__ stats,
-                                                        int64_t ld_stats, int64_t* __restrict__ zero_stats, int64_t n_zero) {
-  __shared__ float red[2][4];
-  const int r = blockIdx.x;  // b*q_len + i
-  const int b = r / q_len, i = r - b * q_len;
-  const int p = *cur_len - q_len + i;
-  const int64_t id = ids[(int64_t)b * ids_stride + p];
-  float s = 0.f, s2 = 0.f;
   for (int c = threadIdx.x; c < d; c += blockDim.x) {
     const float v = TypeIO<TW>::ld(tok + id * d + c) + TypeIO<TW>::ld(pos + (int64_t)p * d + c);
     h[(int64_t)r * d + c] = v;
-    hb[(int64_t)r * d + c] = f2bf(v);
-    s += v;
-    s2 += v * v;
+    if (hb) hb[(int64_t)r * d + c] = f2bf(v);
   }
-  s = wave_sum(s);
-  s2 = wave_sum(s2);
-  if ((threadIdx.x & 63) == 0) {
-    red[0][threadIdx.x >> 6] = s;
-    red[1][threadIdx.x >> 6] = s2;
-  }
-  __syncthreads();
-  if (threadIdx.x < 2 * KW_LN_GROUPS) {
-    int64_t v = 0;
-    if (threadIdx.x == 0) v = llrint((double)((red[0][0] + red[0][1]) + (red[0][2] + red[0][3])) * 4294967296.0);
-    if (threadIdx.x == 1) v = llrint((double)((red[1][0] + red[1][1]) + (red[1][2] + red[1][3])) * 268435456.0);
-    stats[(int64_t)r * ld_stats + threadIdx.x] = v;
-  }
-  for (int64_t z = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; z < n_zero; z += (int64_t)gridDim.x * blockDim.x)
-    zero_stats[z] = 0;
 }
 
 }  // namespace
@@ -170,38 +134,17 @@ extern "C" int kw_mel_to_time_major(const float* mel, int64_t B, int64_t C, int6
 
 extern "C" int kw_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
                         const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
-                        kw_stream_t stream) {
+                        void* hb, kw_stream_t stream) {
   if (!ids || !cur_len || !tok_emb || !pos_emb || !h || B <= 0 || q_len <= 0 || d <= 0)
     return kw_set_error_msg(KW_EINVAL, "kw_embed: invalid arguments");
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)(B * q_len));
   if (dtype == KW_DT_F32)
     hipLaunchKernelGGL(embed_kernel<float>, grid, dim3(256), 0, s, ids, ids_stride, (int)q_len, cur_len,
-                       (const float*)tok_emb, (const float*)pos_emb, (int)d, h);
+                       (const float*)tok_emb, (const float*)pos_emb, (int)d, h, (bf16_t*)hb);
   else
     hipLaunchKernelGGL(embed_kernel<bf16_t>, grid, dim3(256), 0, s, ids, ids_stride, (int)q_len, cur_len,
-                       (const bf16_t*)tok_emb, (const bf16_t*)pos_emb, (int)d, h);
-  KW_CHECK_LAUNCH();
-  return KW_OK;
-}
-
-extern "C" int kw_dec_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64_t q_len,
-                            const int32_t* cur_len, const void* tok_emb, const void* pos_emb, int64_t d, float* h,
-                            void* hb, int64_t* stats, int64_t ld_stats, int64_t* zero_stats, int64_t n_zero,
-                            kw_stream_t stream) {
-  if (!ids || !cur_len || !tok_emb || !pos_emb || !h || !hb || !stats || B <= 0 || q_len <= 0 || d <= 0 ||
-      ld_stats < 2 * KW_LN_GROUPS || n_zero < 0 || (n_zero > 0 && !zero_stats))
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_embed: invalid arguments");
-  hipStream_t s = (hipStream_t)stream;
-  dim3 grid((unsigned)(B * q_len));
-  if (dtype == KW_DT_F32)
-    hipLaunchKernelGGL(dec_embed_kernel<float>, grid, dim3(256), 0, s, ids, ids_stride, (int)q_len, cur_len,
-                       (const float*)tok_emb, (const float*)pos_emb, (int)d, h, (bf16_t*)hb, stats, ld_stats, zero_stats,
-                       n_zero);
-  else
-    hipLaunchKernelGGL(dec_embed_kernel<bf16_t>, grid, dim3(256), 0, s, ids, ids_stride, (int)q_len, cur_len,
-                       (const bf16_t*)tok_emb, (const bf16_t*)pos_emb, (int)d, h, (bf16_t*)hb, stats, ld_stats,
-                       zero_stats, n_zero);
+                       (const bf16_t*)tok_emb, (const bf16_t*)pos_emb, (int)d, h, (bf16_t*)hb);
   KW_CHECK_LAUNCH();
   return KW_OK;
 }

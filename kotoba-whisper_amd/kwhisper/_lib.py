@@ -38,16 +38,13 @@ class GemmArgs(ctypes.Structure):
     ]
 
 
-KW_LN_GROUPS = 8
-
-
 class DecLinearArgs(ctypes.Structure):
     _fields_ = [
-        ("x", c_vp), ("ldx", c_i64), ("ln_stats", c_vp), ("ld_stats", c_i64), ("ln_eps", ctypes.c_float),
+        ("x", c_vp), ("ldx", c_i64), ("ln", ctypes.c_int), ("ln_eps", ctypes.c_float),
         ("ln_colsum", c_vp), ("W", c_vp), ("bias", c_vp), ("epilogue", ctypes.c_int),
         ("C", c_vp), ("ldc", c_i64), ("c_dtype", ctypes.c_int),
         ("gelu", ctypes.c_int), ("scale", ctypes.c_float), ("scale_cols", c_i64),
-        ("h", c_vp), ("hb", c_vp), ("ldh", c_i64), ("stats_out", c_vp),
+        ("h", c_vp), ("hb", c_vp), ("ldh", c_i64),
         ("M", c_i64), ("N", c_i64), ("K", c_i64),
         ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
     ]
@@ -76,13 +73,12 @@ EXPORTS = {
     "kw_dec_linear_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
     "kw_pack_weight": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "kw_packed_weight_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
-    "kw_dec_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp,
-                                    c_vp, c_i64, c_vp, c_i64, c_vp]),
     "kw_layernorm": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp]),
     "kw_attention": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
-    "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp]),
+    "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kw_self_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
-                                         c_vp, c_vp]),
+                                         c_vp, c_vp, ctypes.c_size_t, c_vp]),
+    "kw_self_attn_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64]),
     "kw_cross_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
                                           c_vp, ctypes.c_size_t, c_vp]),
     "kw_cross_attn_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64, c_i64]),

@@ -46,6 +46,8 @@ class DecodeSession:
             for n_, k_ in ((3 * d, d), (d, d), (s.decoder_ffn_dim, d), (d, s.decoder_ffn_dim), (s.vocab_size, d)):
                 ws = max(ws, ops.dec_linear_workspace_bytes(n_, k_))
         self.lin_ws = torch.zeros(((ws + 3) // 4,), device=dev, dtype=torch.float32) if ws else None
+        self.self_ws = torch.zeros((ops.self_attn_workspace_bytes(B, H, T_MAX) + 3) // 4, device=dev,
+                                   dtype=torch.float32)
         self._graph = None
         self._graph_key = None
         if enc is not None:
@@ -70,12 +72,8 @@ class DecodeSession:
                 ws=torch.zeros((ops.cross_attn_workspace_bytes(self.B, q, self.eng.H, _HD, self.T) // 4 + 1,),
                                device=dev, dtype=torch.float32),
             )
-            if self.eng.packed:
-                # bf16 mirror of the residual stream (the LayerNorm-fused linears' operand) and the
-                # fixed-point statistics of every decoder LayerNorm: [3L+1][rows][2*KW_LN_GROUPS] int64
+            if self.eng.packed:  # bf16 mirror of the residual stream (the LayerNorm-fused linears' operand)
                 self._bufs[q]["hb"] = torch.empty((rows, d), device=dev, dtype=torch.bfloat16)
-                self._bufs[q]["stats"] = torch.zeros((3 * s.decoder_layers + 1, rows, ops.ln_stats_row_words()),
-                                                     device=dev, dtype=torch.int64)
         return self._bufs[q]
 
     def _gemm(self, A, W, C, M, N, K, **kw):
@@ -94,33 +92,29 @@ class DecodeSession:
         eps = s.layer_norm_eps
         if eng.packed:
             # bf16 path: every decoder LayerNorm is fused into the linear that consumes it
-            # (operand = the bf16 residual mirror hb, statistics from the fixed-point accumulators its
-            # producer filled); the residual-add linears update h / hb and fill the next statistics.
-            st, hb, h = b["stats"], b["hb"], b["h"]
-            G2 = ops.ln_stats_row_words()
+            # (operand = the bf16 residual mirror hb, its rows' statistics computed in that kernel); the
+            # residual-add linears update h and hb.
+            hb, h = b["hb"], b["h"]
             ws = self.lin_ws
             lin = ops.DecLinearPlan
-            seq = [("dembed", q, h, hb, st[0], st[1:])]
+            seq = [("embed", q, h, hb)]
             for li, lay in enumerate(eng.dec_layers):
-                k = 3 * li
-                seq.append(lin(hb, lay["qkv_w"], rows, 3 * d, d, ln=(st[k], 0, G2, eps, lay["qkv_cs"]), bias=lay["qkv_b"],
+                seq.append(lin(hb, lay["qkv_w"], rows, 3 * d, d, ln=(eps, lay["qkv_cs"]), bias=lay["qkv_b"],
                                C=b["qkv"], scale=scale, scale_cols=d, workspace=ws))
                 seq.append(("self", q, b["qkv"], li, b["attn"]))
-                seq.append(lin(b["attn"], lay["o_w"], rows, d, d, bias=lay["o_b"], resid=(h, hb, d, 0),
-                               stats_out=(st[k + 1], 0, G2), workspace=ws))
-                seq.append(lin(hb, lay["xq_w"], rows, d, d, ln=(st[k + 1], 0, G2, eps, lay["xq_cs"]), bias=lay["xq_b"],
+                seq.append(lin(b["attn"], lay["o_w"], rows, d, d, bias=lay["o_b"], resid=(h, hb, d, 0), workspace=ws))
+                seq.append(lin(hb, lay["xq_w"], rows, d, d, ln=(eps, lay["xq_cs"]), bias=lay["xq_b"],
                                C=b["qx"], scale=scale, scale_cols=d, workspace=ws))
                 seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
                 seq.append(lin(b["attn"], lay["xo_w"], rows, d, d, bias=lay["xo_b"], resid=(h, hb, d, 0),
-                               stats_out=(st[k + 2], 0, G2), workspace=ws))
-                seq.append(lin(hb, lay["fc1_w"], rows, s.decoder_ffn_dim, d, ln=(st[k + 2], 0, G2, eps, lay["fc1_cs"]),
+                               workspace=ws))
+                seq.append(lin(hb, lay["fc1_w"], rows, s.decoder_ffn_dim, d, ln=(eps, lay["fc1_cs"]),
                                bias=lay["fc1_b"], C=b["ffn"], gelu=True, workspace=ws))
                 seq.append(lin(b["ffn"], lay["fc2_w"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
-                               resid=(h, hb, d, 0), stats_out=(st[k + 3], 0, G2), workspace=ws))
+                               resid=(h, hb, d, 0), workspace=ws))
             # final LayerNorm (folded into the packed LM head) + proj_out on the last position of every row
-            Ld = s.decoder_layers
             seq.append(lin(hb, eng.lm_w, B, s.vocab_size, d, ldx=q * d, x_offset=(q - 1) * d,
-                           ln=(st[3 * Ld], (q - 1) * G2, q * G2, eps, eng.lm_cs), bias=eng.lm_b, C=self.logits, workspace=ws))
+                           ln=(eps, eng.lm_cs), bias=eng.lm_b, C=self.logits, workspace=ws))
             self._plans[q] = seq
             return seq
         seq = [("embed", q, b["h"])]
@@ -156,12 +150,10 @@ class DecodeSession:
             if k == "ln":
                 ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4])
             elif k == "embed":
-                ops.embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2])
-            elif k == "dembed":
-                ops.dec_embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2], p[3], p[4], p[5])
+                ops.embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2], p[3] if len(p) > 3 else None)
             elif k == "self":
                 _, q, qkv, li, out = p
-                ops.self_attn_step(qkv, B, q, H, _HD, self.kc[li], self.vc[li], T_MAX, self.cur_len, out)
+                ops.self_attn_step(qkv, B, q, H, _HD, self.kc[li], self.vc[li], T_MAX, self.cur_len, out, self.self_ws)
             elif k == "cross":
                 _, q, qx, li, out, ws = p
                 ops.cross_attn_step(qx, B, q, H, _HD, self.cross[2 * li], self.cross[2 * li + 1], self.T, out, ws)

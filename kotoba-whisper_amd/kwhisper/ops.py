@@ -126,22 +126,16 @@ def dec_linear_workspace_bytes(N: int, K: int) -> int:
     return int(_lib().kw_dec_linear_workspace_bytes(N, K))
 
 
-def ln_stats_row_words() -> int:
-    """int64 words per row of a fixed-point LayerNorm statistics buffer (include/kwhisper.h)."""
-    return 2 * L.KW_LN_GROUPS
-
-
 class DecLinearPlan:
     """A pre-built ``kw_dec_linear`` call (decode-step linear over packed weights).
 
-    ``x``: bf16 [M][ldx] activations (x_offset elements from the start); ``ln`` = (stats int64 tensor,
-    word offset, ld_stats, eps, colsum f32 [N]) fuses the LayerNorm of x (gamma/beta folded into W/bias
-    by the caller, colsum = row sums of the folded bf16 weight: ``ln_colsum``);
-    STORE writes ``C`` (f32 or bf16, ldc); RESID updates ``resid`` = (h f32, hb bf16 mirror, ldh, row
-    offset) and adds the next LayerNorm's statistics into ``stats_out`` = (tensor, word offset, ld_stats)."""
+    ``x``: bf16 [M][ldx] activations (x_offset elements from the start); ``ln`` = (eps, colsum f32 [N])
+    fuses the LayerNorm of x's rows (gamma/beta folded into W/bias by the caller, colsum = row sums of
+    the folded bf16 weight: ``ln_colsum``); STORE writes ``C`` (f32 or bf16, ldc); RESID updates
+    ``resid`` = (h f32, hb bf16 mirror, ldh, row offset)."""
 
     def __init__(self, x, W, M, N, K, *, ldx=None, x_offset=0, ln=None, bias=None, C=None, ldc=None, c_offset=0,
-                 gelu=False, scale=1.0, scale_cols=0, resid=None, stats_out=None, workspace=None):
+                 gelu=False, scale=1.0, scale_cols=0, resid=None, workspace=None):
         _cuda(x, W, bias, C, workspace)
         if x.dtype != torch.bfloat16 or W.dtype != torch.bfloat16:
             raise ValueError("kw_dec_linear takes bf16 activations and packed bf16 weights")
@@ -151,19 +145,15 @@ class DecLinearPlan:
         keep = [x, W, bias, C, workspace]
         a.x = x.data_ptr() + x_offset * 2
         a.ldx = K if ldx is None else ldx
-        a.ld_stats = ln_stats_row_words()
         if ln is not None:
-            st, off, ld, eps, colsum = ln
-            _cuda(st, colsum)
-            if st.dtype != torch.int64:
-                raise ValueError("LayerNorm statistics are int64 fixed point")
+            eps, colsum = ln
+            _cuda(colsum)
             if colsum.dtype != torch.float32 or colsum.numel() < N:
                 raise ValueError("ln colsum must be float32 [N]")
-            a.ln_stats = st.data_ptr() + off * 8
-            a.ld_stats = ld
+            a.ln = 1
             a.ln_eps = float(eps)
             a.ln_colsum = colsum.data_ptr()
-            keep += [st, colsum]
+            keep.append(colsum)
         a.W = W.data_ptr()
         a.bias = bias.data_ptr() if bias is not None else None
         if resid is not None:
@@ -176,14 +166,6 @@ class DecLinearPlan:
             a.hb = hb.data_ptr() + row0 * ldh * 2
             a.ldh = ldh
             keep += [h, hb]
-            if stats_out is not None:
-                so, soff, sld = stats_out
-                _cuda(so)
-                if so.dtype != torch.int64:
-                    raise ValueError("LayerNorm statistics are int64 fixed point")
-                a.stats_out = so.data_ptr() + soff * 8
-                a.ld_stats = sld
-                keep.append(so)
         else:
             if C is None:
                 raise ValueError("STORE needs C")
@@ -236,26 +218,23 @@ def attention(qkv: torch.Tensor, B: int, H: int, T: int, hd: int, out: torch.Ten
     return out
 
 
-def embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h):
-    _cuda(ids, cur_len, tok_emb, pos_emb, h)
+def embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h, hb=None):
+    """Decoder embedding into the f32 residual h (and its bf16 mirror hb for the bf16 engine)."""
+    _cuda(ids, cur_len, tok_emb, pos_emb, h, hb)
     L.check(_lib().kw_embed(_dt(tok_emb), _p(ids), ids.stride(0), B, q_len, _p(cur_len), _p(tok_emb), _p(pos_emb),
-                            tok_emb.shape[1], _p(h), _s()), "kw_embed")
+                            tok_emb.shape[1], _p(h), _p(hb), _s()), "kw_embed")
 
 
-def dec_embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h, hb, stats, zero_stats=None):
-    """Embedding for the bf16 decode step: h, its bf16 mirror hb, the first LayerNorm's statistics
-    (``stats`` int64 [B*q_len][2*KW_LN_GROUPS]) and zeroing of the later accumulators ``zero_stats``."""
-    _cuda(ids, cur_len, tok_emb, pos_emb, h, hb, stats, zero_stats)
-    nz = zero_stats.numel() if zero_stats is not None else 0
-    L.check(_lib().kw_dec_embed(_dt(tok_emb), _p(ids), ids.stride(0), B, q_len, _p(cur_len), _p(tok_emb),
-                                _p(pos_emb), tok_emb.shape[1], _p(h), _p(hb), _p(stats), stats.stride(0),
-                                _p(zero_stats), nz, _s()), "kw_dec_embed")
+def self_attn_workspace_bytes(B, H, t_max) -> int:
+    return int(_lib().kw_self_attn_workspace(B, H, t_max))
 
 
-def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out):
-    _cuda(qkv, k_cache, v_cache, cur_len, out)
+def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out, workspace=None):
+    """Static-cache self-attention; q_len == 1 needs a zero-filled ``workspace`` (self_attn_workspace_bytes)."""
+    _cuda(qkv, k_cache, v_cache, cur_len, out, workspace)
+    nb = workspace.numel() * workspace.element_size() if workspace is not None else 0
     L.check(_lib().kw_self_attn_step(_dt(qkv), _p(qkv), B, q_len, H, hd, _p(k_cache), _p(v_cache), t_max,
-                                     _p(cur_len), _p(out), _s()), "kw_self_attn_step")
+                                     _p(cur_len), _p(out), _p(workspace), nb, _s()), "kw_self_attn_step")
 
 
 def cross_attn_workspace_bytes(B, q_len, H, hd, S) -> int:
