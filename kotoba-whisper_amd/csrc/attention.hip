@@ -346,28 +346,29 @@ __device__ __forceinline__ void attend_rows(const float qv[8], int k0, int k1, K
 // (256 threads = 32 key slots x 8 lanes; lane (slot, sub) holds 16 B of rows slot, slot+32, ...).
 // Returns the chunk's (m, l) to every thread and the unnormalised o[tid] to threads 0..63.
 // ------------------------------------------------------------------------------------------------
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 template <typename T>
 struct Row8 {
-  uint4 u[sizeof(T) == 2 ? 1 : 2];
+  u32x4 u[sizeof(T) == 2 ? 1 : 2];
 };
 template <typename T>
-__device__ __forceinline__ Row8<T> ld_row8(const T* p) {
+__device__ __forceinline__ Row8<T> ld_row8(const T* p) {  // streamed once per step: non-temporal
   Row8<T> r;
-  r.u[0] = *reinterpret_cast<const uint4*>(p);
-  if constexpr (sizeof(T) == 4) r.u[1] = reinterpret_cast<const uint4*>(p)[1];
+  r.u[0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+  if constexpr (sizeof(T) == 4) r.u[1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + 1);
   return r;
 }
 template <typename T>
 __device__ __forceinline__ void unpack8(const Row8<T>& r, float v[8]) {
   if constexpr (sizeof(T) == 2) {
-    const uint32_t w[4] = {r.u[0].x, r.u[0].y, r.u[0].z, r.u[0].w};
+    const uint32_t w[4] = {r.u[0][0], r.u[0][1], r.u[0][2], r.u[0][3]};
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       v[2 * i] = __uint_as_float(w[i] << 16);
       v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
   } else {
-    const uint32_t w[8] = {r.u[0].x, r.u[0].y, r.u[0].z, r.u[0].w, r.u[1].x, r.u[1].y, r.u[1].z, r.u[1].w};
+    const uint32_t w[8] = {r.u[0][0], r.u[0][1], r.u[0][2], r.u[0][3], r.u[1][0], r.u[1][1], r.u[1][2], r.u[1][3]};
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = __uint_as_float(w[i]);
   }
