@@ -1,7 +1,7 @@
 """Oracle Whisper generate (greedy) -- TEST INFRASTRUCTURE ONLY (see oracle/__init__.py).
 
-A pure-Python/numpy restatement of ``WhisperGenerationMixin.generate`` for
-``num_beams == 1`` (transformers 5.15.0, TF/models/whisper/generation_whisper.py):
+A pure-Python/numpy restatement of ``WhisperGenerationMixin.generate`` (transformers 5.15.0,
+TF/models/whisper/generation_whisper.py), greedy and beam search:
 
   * prompt:       ``_retrieve_init_tokens``           :1455-1608 (+ ``detect_language`` :1620-1674)
   * processors:   ``_retrieve_logit_processors``       :1774-1812
@@ -12,6 +12,11 @@ A pure-Python/numpy restatement of ``WhisperGenerationMixin.generate`` for
                   ``_get_input_segment`` :1847, ``_set_max_new_tokens_and_length`` :1920-1946)
   * greedy:       ``GenerationMixin._sample``  TF/generation/utils.py:2783-2941 (argmax first-max,
                   finished rows -> pad :2929, MaxLength / EOS stopping ``stopping_criteria.py:75-77``)
+  * beam search:  ``GenerationMixin._beam_search``  TF/generation/utils.py:3208-3527 with
+                  ``_get_top_k_continuations`` :3077, ``_get_running_beams_for_next_iteration`` :3131,
+                  ``_update_finished_beams`` :3153, ``_check_early_stop_heuristic`` :3008,
+                  ``_beam_search_has_unfinished_sequences`` :3055; processors act on log-probs
+                  (log_softmax first, :3380-3381); inputs expanded x num_beams
   * postprocess:  ``generate_with_fallback`` :1042-1086 (strip prompt, pad-count quirk, strip EOS),
                   ``_retrieve_segment`` :1977-2074, ``_pad_to_max_length`` :126-237 (right pad)
 """
@@ -131,6 +136,104 @@ def greedy(model: WhisperNP, enc: np.ndarray, prompt: np.ndarray, gen: dict, max
     return ids
 
 
+def _log_softmax(x: np.ndarray) -> np.ndarray:
+    """torch.nn.functional.log_softmax in fp32: x - max - log(sum(exp(x - max)))."""
+    x = x.astype(np.float32)
+    m = x.max(-1, keepdims=True)
+    lse = np.log(np.exp((x - m).astype(np.float64)).sum(-1, keepdims=True)).astype(np.float32)
+    return ((x - m) - lse).astype(np.float32)
+
+
+def _topk(x: np.ndarray, k: int) -> np.ndarray:
+    """Indices of torch.topk(x, k) along the last axis (descending; ties -> lower index first)."""
+    return np.argsort(-x, axis=-1, kind="stable")[..., :k]
+
+
+def _take(a: np.ndarray, idx: np.ndarray) -> np.ndarray:
+    """``_gather_beams`` (utils.py:2988): take_along_dim on axis 1."""
+    while idx.ndim < a.ndim:
+        idx = idx[..., None]
+    return np.take_along_axis(a, idx, axis=1)
+
+
+def beam_search(model: WhisperNP, enc: np.ndarray, prompt: np.ndarray, gen: dict, max_length: int,
+                begin_index: int, return_timestamps: bool, num_beams: int, length_penalty: float = 1.0,
+                early_stopping=False) -> np.ndarray:
+    """``GenerationMixin._beam_search`` (utils.py:3208-3527), num_return_sequences = 1.
+    Returns (B, prompt + generated) ids of the best beam per item, filled with pad_token_id."""
+    f32 = np.float32
+    NEG = f32(-1.0e9)
+    pad, eos = gen["pad_token_id"], gen["eos_token_id"]
+    B, P = prompt.shape
+    nb = num_beams
+    keep = 2 * nb  # max(2, 1 + n_eos) * num_beams with one EOS id (:3289)
+    fill = pad if pad is not None else eos
+    running = np.full((B, nb, max_length), fill, dtype=np.int64)
+    running[:, :, :P] = prompt[:, None, :]
+    sequences = running.copy()
+    run_scores = np.zeros((B, nb), f32)
+    run_scores[:, 1:] = NEG
+    beam_scores = np.full((B, nb), NEG, f32)
+    fin = np.zeros((B, nb), bool)
+    unsat = np.ones((B, 1), bool)
+    run_bi = np.full((B, nb, max_length - P), -1, np.int32)
+    beam_idx = run_bi.copy()
+    top_mask = np.arange(keep) < nb
+    cache = model.new_cache(np.repeat(enc, nb, axis=0))
+    logits = model.decode(np.repeat(prompt, nb, axis=0), cache)[:, -1]
+    V = logits.shape[-1]
+    cur_len = P
+    while True:
+        flat_hist = running.reshape(B * nb, max_length)[:, :cur_len]
+        lp = process_logits(flat_hist, _log_softmax(logits), gen, begin_index, return_timestamps)
+        lp = (lp.reshape(B, nb, V) + run_scores[:, :, None]).astype(f32).reshape(B, nb * V)
+        # c. top-K continuations (:3077-3129)
+        idx = _topk(lp, keep)
+        topk_lp = np.take_along_axis(lp, idx, axis=1)
+        cur_beam = idx // V
+        tok = idx % V
+        topk_bi = _take(run_bi, cur_beam).copy()
+        topk_seq = _take(running, cur_beam).copy()
+        topk_seq[:, :, cur_len] = tok
+        topk_bi[:, :, cur_len - P] = cur_beam + np.arange(B)[:, None] * nb
+        # d. stopping criteria: MaxLength on the new length, EOS on the new token
+        hits = np.full((B, keep), cur_len + 1 >= max_length) | (tok == eos)
+        # e. running beams (:3131-3151)
+        trl = (topk_lp + hits.astype(f32) * NEG).astype(f32)
+        nidx = _topk(trl, nb)
+        running = _take(topk_seq, nidx)
+        run_scores = np.take_along_axis(trl, nidx, axis=1)
+        run_bi = _take(topk_bi, nidx)
+        # f. finished beams (:3153-3205)
+        did = hits & top_mask[None, :]
+        tl = (topk_lp / f32((cur_len + 1 - P) ** length_penalty)).astype(f32)
+        full = np.all(fin, axis=-1, keepdims=True) & (early_stopping is True)
+        tl = tl + full.astype(f32) * NEG
+        tl = tl + (~unsat).astype(f32) * NEG
+        tl = (tl + (~did).astype(f32) * NEG).astype(f32)
+        m_seq = np.concatenate([sequences, topk_seq], 1)
+        m_scores = np.concatenate([beam_scores, tl], 1)
+        m_bi = np.concatenate([beam_idx, topk_bi], 1)
+        m_fin = np.concatenate([fin, did], 1)
+        midx = _topk(m_scores, nb)
+        sequences, beam_scores = _take(m_seq, midx), np.take_along_axis(m_scores, midx, axis=1)
+        beam_idx, fin = _take(m_bi, midx), np.take_along_axis(m_fin, midx, axis=1)
+        # g. cache reorder, early-stop heuristic (:3008-3053), loop condition (:3055-3075)
+        model.reorder(cache, run_bi[..., cur_len - P].reshape(-1))
+        cur_len += 1
+        bhl = (max_length - P) if (early_stopping == "never" and length_penalty > 0.0) else (cur_len - P)
+        best_run = (run_scores[:, :1] / f32(bhl ** length_penalty)).astype(f32)
+        worst_fin = np.where(fin, beam_scores.min(1, keepdims=True), NEG)
+        unsat = unsat & np.any(best_run > worst_fin, axis=-1, keepdims=True)
+        go = unsat.any() and not (fin.all() and early_stopping is True) and not hits.all()
+        if not go:
+            break
+        logits = model.decode(running.reshape(B * nb, max_length)[:, cur_len - 1: cur_len], cache)[:, -1]
+    best_bi = beam_idx[:, 0]
+    max_gen = int(((best_bi + 1) != 0).sum(1).max())
+    return sequences[:, 0, : P + max_gen]
+
+
 def _retrieve_segment(seq, ts_begin, seek_num_frames, time_offset, input_stride=2, time_precision=0.02,
                       time_precision_features=0.01):
     ts = seq >= ts_begin
@@ -167,8 +270,8 @@ def _retrieve_segment(seq, ts_begin, seek_num_frames, time_offset, input_stride=
 
 def generate(model: WhisperNP, input_features: np.ndarray, gen: dict, *, max_length=None, language=None,
              task=None, return_timestamps=None, attention_mask=None, return_dict_in_generate=False,
-             return_segments=False, record=None):
-    """Greedy ``WhisperGenerationMixin.generate`` restated (num_beams == 1)."""
+             return_segments=False, record=None, num_beams=1, length_penalty=1.0, early_stopping=False):
+    """``WhisperGenerationMixin.generate`` restated: greedy (num_beams == 1) or beam search."""
     gen = copy.deepcopy(gen)
     feats = np.asarray(input_features, dtype=np.float32)
     b, _, total = feats.shape
@@ -221,7 +324,11 @@ def generate(model: WhisperNP, input_features: np.ndarray, gen: dict, *, max_len
         max_length = min(max_length + min(model.s.max_target_positions // 2 - 1, prompt.shape[1]),
                          model.s.max_target_positions)
         enc = model.encode(seg_in)
-        ids = greedy(model, enc, prompt, gen, max_length, prompt.shape[1], return_timestamps, record)
+        if num_beams > 1:
+            ids = beam_search(model, enc, prompt, gen, max_length, prompt.shape[1], return_timestamps, num_beams,
+                              length_penalty, early_stopping)
+        else:
+            ids = greedy(model, enc, prompt, gen, max_length, prompt.shape[1], return_timestamps, record)
         last_outputs = ids
         pad, eos = gen["pad_token_id"], gen["eos_token_id"]
         for i, p in enumerate(batch_map):

@@ -41,4 +41,24 @@ TINY_MODES = {
     "greedy_translate": (dict(language="ja", task="translate", return_timestamps=False), None),
     "greedy_detect": (dict(return_timestamps=False), None),
     "greedy_short": (dict(BASE, return_timestamps=False, max_length=16), None),
+    "beam5": (dict(BASE, return_timestamps=False, num_beams=5, max_length=24), None),
 }
+
+
+# tools/make_fixtures.py BEAM_MODES: name -> (generate kwargs, eos override)
+BEAM_MODES = {
+    "beam5_ts": (dict(BASE, return_timestamps=True, num_beams=5, max_length=40), None),
+    "beam3_eos": (dict(BASE, return_timestamps=False, num_beams=3, max_length=40), 7656),
+    "beam4_eos_lp_es": (dict(BASE, return_timestamps=False, num_beams=4, max_length=40, length_penalty=0.5,
+                             early_stopping=True), 7656),
+    "beam2_eos_never": (dict(BASE, return_timestamps=False, num_beams=2, max_length=40, length_penalty=2.0,
+                             early_stopping="never"), 20779),
+    "beam3_eos_ts": (dict(BASE, return_timestamps=True, num_beams=3, max_length=40), 7656),
+}
+
+
+def beam_gen_dict(shape, eos=None) -> dict:
+    d = gen_dict(shape)
+    if eos is not None:
+        d["eos_token_id"] = eos
+    return d

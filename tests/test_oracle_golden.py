@@ -11,7 +11,7 @@ from oracle import generate as og
 from oracle.mel import log_mel, mel_filters
 from oracle.whisper_np import WhisperNP
 
-from _util import TINY_MODES, audio_cases, gen_dict, oracle_features, segments_of
+from _util import BEAM_MODES, TINY_MODES, audio_cases, beam_gen_dict, gen_dict, oracle_features, segments_of
 
 STRIDE = 17
 
@@ -79,6 +79,18 @@ def test_oracle_tiny_generate(gold, tiny, mode):
     max_length = kw.pop("max_length", int(g["max_length"]))
     res = og.generate(tiny, feats, gen_dict(TINY, pad), max_length=max_length, **kw)
     toks = res["sequences"] if isinstance(res, dict) else res
+    np.testing.assert_array_equal(toks, g[f"{mode}_tokens"])
+
+
+@pytest.mark.parametrize("mode", sorted(BEAM_MODES))
+def test_oracle_tiny_beam(gold, tiny, mode):
+    """Beam search restatement vs HF generate (num_beams 2-5, EOS finishing, length penalty,
+    early_stopping True / "never", timestamps)."""
+    g = gold("tiny_beam_fp32")
+    kw, eos = BEAM_MODES[mode]
+    kw = dict(kw)
+    feats = oracle_features(TINY, g["cases"])
+    toks = og.generate(tiny, feats, beam_gen_dict(TINY, eos), max_length=kw.pop("max_length"), **kw)
     np.testing.assert_array_equal(toks, g[f"{mode}_tokens"])
 
 

@@ -144,6 +144,36 @@ def model_fixtures(shape, tag, cases, max_length, modes, enc_rows=50):
     print(f"{tag} fixtures done in {time.time() - t0:.1f}s")
 
 
+BEAM_MODES = [
+    # name, generate kwargs, eos override (a token the random-init tiny model emits often, so beams finish)
+    ("beam5_ts", dict(return_timestamps=True, num_beams=5, max_length=40), None),
+    ("beam3_eos", dict(return_timestamps=False, num_beams=3, max_length=40), 7656),
+    ("beam4_eos_lp_es", dict(return_timestamps=False, num_beams=4, max_length=40, length_penalty=0.5,
+                             early_stopping=True), 7656),
+    ("beam2_eos_never", dict(return_timestamps=False, num_beams=2, max_length=40, length_penalty=2.0,
+                             early_stopping="never"), 20779),
+    ("beam3_eos_ts", dict(return_timestamps=True, num_beams=3, max_length=40), 7656),
+]
+
+
+def beam_fixtures():
+    """tests/golden/tiny_beam_fp32.npz: beam search through the real HF generate (tiny, fp32)."""
+    t0 = time.time()
+    m = hf_model(TINY)
+    cases = [("dummy", 0), ("dummy", 1), ("tone", 0), ("tone", 1)]
+    feats = features(TINY.num_mel_bins, cases)
+    out = {"cases": np.array([f"{k}:{s}" for k, s in cases])}
+    for name, kw, eos in BEAM_MODES:
+        gconf, _ = hf_gen_config(TINY)
+        if eos is not None:
+            gconf.eos_token_id = eos
+        m.generation_config = gconf
+        res = run_generate(m, feats, language="ja", task="transcribe", **kw)
+        out[f"{name}_tokens"] = res.numpy().astype(np.int64)
+        print(f"  tiny_beam:{name} {tuple(res.shape)} ({time.time() - t0:.1f}s)")
+    np.savez_compressed(os.path.join(GOLD, "tiny_beam_fp32.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
@@ -166,6 +196,8 @@ def main():
         {"name": "greedy_short", "kw": dict(base, return_timestamps=False, max_length=16)},
         {"name": "beam5", "kw": dict(base, return_timestamps=False, num_beams=5, max_length=24)},
     ]
+    if a.only in (None, "beam"):
+        beam_fixtures()
     if a.only in (None, "tiny"):
         cases = [("dummy", 0), ("dummy", 1), ("tone", 0), ("tone", 1)]
         model_fixtures(TINY, "tiny_fp32", cases, 128, tiny_modes)
