@@ -131,7 +131,7 @@ def main():
 
     # ---- per-kernel measurements (HIP events on the launching stream, after the timed region) ----
     eng = model.engine
-    sess = model._sessions[B]
+    sess = model._sessions[(B, 1)]
     stream = torch.cuda.current_stream(dev)
     iters = a.kernel_iters
 

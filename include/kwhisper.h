@@ -141,10 +141,13 @@ int kw_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64_t B, int64
  * appends k/v of the q_len newest positions [L-q_len, L) to k_cache/v_cache [B][H][t_max][hd],
  * then causal attention for those positions. qkv: [B*q_len][3*H*hd]; out [B*q_len][H*hd]; t_max <= 512.
  * q_len == 1 needs workspace >= kw_self_attn_workspace(B, H, t_max) bytes, zero-filled before first use
- * (arrival counters every call leaves at zero); q_len > 1 ignores it. */
+ * (arrival counters every call leaves at zero); q_len > 1 ignores it.  bp (q_len == 1 only, or NULL):
+ * beam-search slot table [B][bp_stride] int32 -- key/value position k < L-1 of row b is read from
+ * cache row bp[b][k] (beams share their prefix; the reorder of cache_utils.py:2035-2038 moves no K/V). */
 int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t q_len, int64_t H, int64_t hd,
-                      void* k_cache, void* v_cache, int64_t t_max, const int32_t* cur_len, void* out,
-                      void* workspace, size_t ws_bytes, kw_stream_t stream);
+                      void* k_cache, void* v_cache, int64_t t_max, const int32_t* cur_len,
+                      const int32_t* bp, int64_t bp_stride, void* out, void* workspace, size_t ws_bytes,
+                      kw_stream_t stream);
 size_t kw_self_attn_workspace(int64_t B, int64_t H, int64_t t_max);
 
 /* Decoder cross-attention against cached encoder K/V [B][H][S][hd] (TF modeling_whisper.py:323-326).
@@ -181,6 +184,76 @@ typedef struct {
 } kw_sampler_args;
 
 int kw_greedy_step(const kw_sampler_args* args, kw_stream_t stream);
+
+/* ---- beam search step (a10: TF/generation/utils.py:3208-3527), num_return_sequences = 1 ----------
+ * Running rows are R = B * num_beams, item-major (row = b * num_beams + beam).  One step is
+ * kw_beam_logprobs then kw_beam_select; both read the device cur_len and do nothing once *done != 0,
+ * so the step can be replayed from a hipGraph past the end of the search. */
+
+/* log_softmax of each row's raw f32 logits (utils.py:3380), the Whisper processors on the log-probs
+ * (as kw_greedy_step, with the row's own history ids[r][0..L) ), and the row's k best processed
+ * log-probs, descending, ties to the lower token id: cand_val/cand_idx [R][k], k <= 16. */
+typedef struct {
+  const float* logits;
+  int64_t R, V;
+  const uint8_t* suppress_mask;
+  const int32_t* begin_suppress;
+  int32_t n_begin_suppress;
+  int32_t return_timestamps;
+  int32_t ts_begin, no_ts_id, eos_id;
+  int32_t max_initial_ts;     /* -1 = None */
+  const int64_t* ids;         /* [R][ids_stride] running histories */
+  int64_t ids_stride;
+  const int32_t* cur_len;
+  int32_t begin_index;
+  int32_t k;
+  float* cand_val;
+  int32_t* cand_idx;
+  const int32_t* done;
+} kw_beam_logprobs_args;
+
+int kw_beam_logprobs(const kw_beam_logprobs_args* args, kw_stream_t stream);
+
+/* Selection for one step (utils.py:3077-3205, 3008-3075): top 2*num_beams continuations over
+ * beams x vocab of (log-prob + running score), MaxLength / EOS criteria, the next running beams
+ * (ids rows rewritten in place: parent history + token; bp rows: parent slot table + own slot),
+ * the finished set (fin_seq/fin_score/fin_len/fin_flag, length_penalty, early_stopping 0 = False,
+ * 1 = True, 2 = "never"), the early-stop heuristic (unsat) and, from the last item, *go (1 = the
+ * reference loop continues) / *done, and *cur_len += 1.  Initial state: ids rows = prompt, bp rows =
+ * own row for p < P (or bp NULL when the K/V cache is not shared), run_scores = [0, -1e9, ...] per
+ * item, fin_seq = fill_id, fin_score = -1e9, fin_len = fin_flag = 0, unsat = 1, counter = go = done = 0.
+ * 2 <= num_beams <= 8, max_length <= 512, fin_stride / ids_stride / bp_stride >= max_length. */
+typedef struct {
+  int64_t B;
+  int32_t num_beams;
+  int64_t V;
+  const float* cand_val;
+  const int32_t* cand_idx;
+  int64_t* ids;
+  int64_t ids_stride;
+  int32_t* bp;
+  int64_t bp_stride;
+  float* run_scores;          /* [R] */
+  int64_t* fin_seq;           /* [B][num_beams][fin_stride] */
+  int64_t fin_stride;
+  float* fin_score;           /* [B][num_beams] */
+  int32_t* fin_len;           /* generated tokens of each finished sequence */
+  int32_t* fin_flag;
+  int32_t* unsat;             /* [B] */
+  int32_t* cur_len;
+  int32_t begin_index;        /* prompt length */
+  int32_t max_length;
+  int32_t eos_id;
+  int32_t fill_id;            /* pad_token_id (or eos when there is none) */
+  float length_penalty;
+  int32_t early_stopping;
+  int32_t* counter;
+  int32_t* go;
+  int32_t* done;
+  int32_t* item_flags;        /* [B][3] scratch */
+} kw_beam_select_args;
+
+int kw_beam_select(const kw_beam_select_args* args, kw_stream_t stream);
 
 #ifdef __cplusplus
 }

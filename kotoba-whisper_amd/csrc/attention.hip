@@ -563,6 +563,7 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q
 template <typename T>
 __global__ __launch_bounds__(256) void self_attn_step1(const T* __restrict__ qkv, int H, T* __restrict__ kc,
                                                        T* __restrict__ vc, int t_max, const int32_t* __restrict__ cur_len,
+                                                       const int32_t* __restrict__ bp, int bp_stride,
                                                        float* __restrict__ ws, int* __restrict__ cnt, T* __restrict__ out) {
   __shared__ float red[4][64];
   __shared__ float stat[8];
@@ -586,9 +587,14 @@ __global__ __launch_bounds__(256) void self_attn_step1(const T* __restrict__ qkv
   float qv[8];
   load8<T>(row + sub * 8, qv);
   float m, l, o;
+  // beam search: position k of this row lives in cache row bp[b][k] (a shared prefix), else in row b
+  const int32_t* bpr = bp ? bp + (int64_t)b * bp_stride : nullptr;
+  auto slot = [&](int k) -> int64_t {
+    return ((int64_t)(bpr ? bpr[k] : b) * H + h) * t_max * HD + (int64_t)k * HD;
+  };
   attend_chunk<T>(qv, k0, min(L, k0 + 256),
-                  [&](int k) -> const T* { return k < p0 ? kb + (int64_t)k * HD : row + d; },
-                  [&](int k) -> const T* { return k < p0 ? vb + (int64_t)k * HD : row + 2 * d; }, red, stat, m, l, o);
+                  [&](int k) -> const T* { return k < p0 ? kc + slot(k) : row + d; },
+                  [&](int k) -> const T* { return k < p0 ? vc + slot(k) : row + 2 * d; }, red, stat, m, l, o);
   T* orow = out + (int64_t)b * d + h * HD;
   if (ns == 1) {
     if (tid < HD) TypeIO<T>::st(orow + tid, o / l);
@@ -631,12 +637,15 @@ extern "C" size_t kw_self_attn_workspace(int64_t B, int64_t H, int64_t t_max) {
 }
 
 extern "C" int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t q_len, int64_t H, int64_t hd,
-                                 void* k_cache, void* v_cache, int64_t t_max, const int32_t* cur_len, void* out,
-                                 void* workspace, size_t ws_bytes, kw_stream_t stream) {
+                                 void* k_cache, void* v_cache, int64_t t_max, const int32_t* cur_len,
+                                 const int32_t* bp, int64_t bp_stride, void* out, void* workspace, size_t ws_bytes,
+                                 kw_stream_t stream) {
   if (!qkv || !k_cache || !v_cache || !cur_len || !out || B <= 0 || q_len <= 0 || H <= 0 || t_max <= 0 || t_max > 512)
     return kw_set_error_msg(KW_EINVAL, "kw_self_attn_step: invalid arguments (t_max <= 512)");
   if (hd != HD) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_self_attn_step: head_dim must be 64");
   hipStream_t s = (hipStream_t)stream;
+  if (bp && (q_len != 1 || bp_stride < t_max))
+    return kw_set_error_msg(KW_EINVAL, "kw_self_attn_step: a slot table needs q_len == 1 and bp_stride >= t_max");
   if (q_len == 1) {
     if (!workspace || ws_bytes < kw_self_attn_workspace(B, H, t_max))
       return kw_set_error_msg(KW_EINVAL, "kw_self_attn_step: needs a zero-filled workspace of kw_self_attn_workspace()");
@@ -645,10 +654,10 @@ extern "C" int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t 
     dim3 grid((unsigned)(B * H), (unsigned)((t_max + 255) / 256));
     if (dtype == KW_DT_BF16)
       hipLaunchKernelGGL(self_attn_step1<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)qkv, (int)H, (bf16_t*)k_cache,
-                         (bf16_t*)v_cache, (int)t_max, cur_len, part, cnt, (bf16_t*)out);
+                         (bf16_t*)v_cache, (int)t_max, cur_len, bp, (int)bp_stride, part, cnt, (bf16_t*)out);
     else
       hipLaunchKernelGGL(self_attn_step1<float>, grid, dim3(256), 0, s, (const float*)qkv, (int)H, (float*)k_cache,
-                         (float*)v_cache, (int)t_max, cur_len, part, cnt, (float*)out);
+                         (float*)v_cache, (int)t_max, cur_len, bp, (int)bp_stride, part, cnt, (float*)out);
   } else if (dtype == KW_DT_BF16) {
     hipLaunchKernelGGL(self_attn_step<bf16_t>, dim3((unsigned)(B * H)), dim3(256), 0, s, (const bf16_t*)qkv, (int)q_len,
                        (int)H, (bf16_t*)k_cache, (bf16_t*)v_cache, (int)t_max, cur_len, (bf16_t*)out);

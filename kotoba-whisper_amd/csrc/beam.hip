@@ -1,0 +1,391 @@
+// Beam search step on device (a10): GenerationMixin._beam_search (TF/generation/utils.py:3208-3527)
+// for one decode step, captured in the same hipGraph as the decoder forward.
+//
+//  kw_beam_logprobs (one 1024-thread workgroup per running row = batch item x beam):
+//    log_softmax of the raw f32 logits (:3380), the Whisper processors on the log-probs (Suppress ->
+//    SuppressAtBegin -> WhisperTimeStamp, processors.h; :3381), and the row's K best processed
+//    log-probs (K = 2 * num_beams: the global top-K over beams x vocab of log-prob + beam score is
+//    always inside the union of the rows' top-K, adding a per-row constant keeps a row's order).
+//  kw_beam_select (one workgroup per batch item):
+//    _get_top_k_continuations (:3077), the MaxLength / EOS stopping criteria on the K continuations,
+//    _get_running_beams_for_next_iteration (:3131), _update_finished_beams (:3153, length penalty,
+//    early_stopping), the cache reorder (:3445-3456) and _check_early_stop_heuristic (:3008) /
+//    _beam_search_has_unfinished_sequences (:3055).  The reorder moves no K/V: every running row
+//    keeps a slot table bp[row][pos] = the cache row that holds its position pos (a beam's history
+//    is its parent's table + its own new slot), so a reorder rewrites nb x L int32 per item
+//    instead of gathering nb x layers x heads x L x 64 K/V values.
+// All arithmetic is fp32 in the reference's order (log-prob + score, -1e9 masks, score /
+// len**length_penalty); every top-k breaks ties by the lower flat index.
+#include <math.h>
+
+#include "processors.h"
+
+namespace {
+
+using namespace kwp;
+
+constexpr int KMAX = 16;  // candidates per row (2 * num_beams <= 16)
+constexpr float NEG = -1.0e9f;
+
+__device__ __forceinline__ bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia < ib); }
+
+__global__ __launch_bounds__(ST) void beam_logprobs_kernel(kw_beam_logprobs_args a) {
+  __shared__ float shf[ST / 64];
+  __shared__ int shi[ST / 64][2];
+  __shared__ RowState st_sh;
+  __shared__ int win_t;
+  if (*a.done) return;
+  const int r = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int L = *a.cur_len;
+  const int V = (int)a.V;
+  const int K = a.k;
+  const float* x = a.logits + (int64_t)r * a.V;
+  const int64_t* ids = a.ids + (int64_t)r * a.ids_stride;
+
+  // log_softmax normaliser of the raw row: lp = (x - max) - log(sum exp(x - max))
+  float m = -INFINITY;
+  for (int v = tid; v < V; v += ST) m = fmaxf(m, x[v]);
+  m = block_reduce_max(m, shf);
+  float s = 0.f;
+  for (int v = tid; v < V; v += ST) s += expf(x[v] - m);
+  s = block_reduce_sum(s, shf);
+  const float ls = logf(s);
+  auto lp = [&](int v) { return (x[v] - m) - ls; };
+
+  int fin = 0;
+  RowState st = row_state(ids, L, a.begin_index, a.ts_begin, a.no_ts_id, a.eos_id, a.return_timestamps,
+                          a.max_initial_ts, &fin, shi, &st_sh);
+  if (st.rt) timestamp_rule(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, V, lp, shf);
+
+  // per-thread sorted top-K of its strided slice, then K rounds of a block arg-max over the heads
+  float tv[KMAX];
+  int ti[KMAX];
+#pragma unroll
+  for (int i = 0; i < KMAX; ++i) {
+    tv[i] = -INFINITY;
+    ti[i] = 0x7fffffff;
+  }
+  for (int v = tid; v < V; v += ST) {
+    const float sv = process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, lp(v));
+    if (!better(sv, v, tv[KMAX - 1], ti[KMAX - 1])) continue;  // (keeps KMAX >= K per thread)
+    // insert (v increases along the slice, so an equal value goes after the existing ones)
+    float cv = sv;
+    int ci = v;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i) {
+      if (better(cv, ci, tv[i], ti[i])) {
+        const float t1 = tv[i];
+        const int t2 = ti[i];
+        tv[i] = cv;
+        ti[i] = ci;
+        cv = t1;
+        ci = t2;
+      }
+    }
+  }
+  int head = 0;
+  for (int k = 0; k < K; ++k) {
+    float hv = -INFINITY;
+    int hi = 0x7fffffff;
+#pragma unroll
+    for (int i = 0; i < KMAX; ++i)
+      if (i == head) {
+        hv = tv[i];
+        hi = ti[i];
+      }
+    float bv = hv;
+    int bi = hi, bt = tid;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int oi = __shfl_xor(bi, o, 64), ot = __shfl_xor(bt, o, 64);
+      if (better(ov, oi, bv, bi)) {
+        bv = ov;
+        bi = oi;
+        bt = ot;
+      }
+    }
+    if ((tid & 63) == 0) {
+      shf[tid >> 6] = bv;
+      shi[tid >> 6][0] = bi;
+      shi[tid >> 6][1] = bt;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float gv = shf[0];
+      int gi = shi[0][0], gt = shi[0][1];
+      for (int w = 1; w < ST / 64; ++w)
+        if (better(shf[w], shi[w][0], gv, gi)) {
+          gv = shf[w];
+          gi = shi[w][0];
+          gt = shi[w][1];
+        }
+      a.cand_val[(int64_t)r * K + k] = gv;
+      a.cand_idx[(int64_t)r * K + k] = gi == 0x7fffffff ? 0 : gi;
+      win_t = gt;
+    }
+    __syncthreads();
+    if (tid == win_t) ++head;
+    __syncthreads();
+  }
+}
+
+// K rounds of a block arg-max over n (value, key) pairs in LDS; writes the winners' positions in order.
+__device__ void block_topk(const float* val, const int* key, int n, int k, int* out_pos, float* shf, int* shi) {
+  const int tid = threadIdx.x;
+  __shared__ int taken[256];
+  for (int i = tid; i < n; i += blockDim.x) taken[i] = 0;
+  __syncthreads();
+  for (int j = 0; j < k; ++j) {
+    float bv = -INFINITY;
+    int bk = 0x7fffffff, bp = -1;
+    for (int i = tid; i < n; i += blockDim.x)
+      if (!taken[i] && (bp < 0 || better(val[i], key[i], bv, bk))) {
+        bv = val[i];
+        bk = key[i];
+        bp = i;
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(bv, o, 64);
+      const int ok = __shfl_xor(bk, o, 64), op = __shfl_xor(bp, o, 64);
+      if (op >= 0 && (bp < 0 || better(ov, ok, bv, bk))) {
+        bv = ov;
+        bk = ok;
+        bp = op;
+      }
+    }
+    if ((tid & 63) == 0) {
+      shf[tid >> 6] = bv;
+      shi[2 * (tid >> 6)] = bk;
+      shi[2 * (tid >> 6) + 1] = bp;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float gv = shf[0];
+      int gk = shi[0], gp = shi[1];
+      for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+        const int wp = shi[2 * w + 1];
+        if (wp >= 0 && (gp < 0 || better(shf[w], shi[2 * w], gv, gk))) {
+          gv = shf[w];
+          gk = shi[2 * w];
+          gp = wp;
+        }
+      }
+      out_pos[j] = gp;
+      taken[gp] = 1;
+    }
+    __syncthreads();
+  }
+}
+
+constexpr int BT = 256;  // beam_select threads
+constexpr int NBMAX = 8;
+constexpr int TMAX = 512;  // history length bound (max_target_positions 448)
+
+__global__ __launch_bounds__(BT) void beam_select_kernel(kw_beam_select_args a) {
+  __shared__ float cval[256];
+  __shared__ int ckey[256];
+  __shared__ float shf[BT / 64];
+  __shared__ int shi[2 * (BT / 64)];
+  __shared__ int top[KMAX], run_pos[NBMAX], fin_pos[NBMAX];
+  __shared__ float t_lp[KMAX], t_run[KMAX], t_fin[KMAX];
+  __shared__ int t_par[KMAX], t_tok[KMAX], t_hit[KMAX];
+  __shared__ float m_val[NBMAX + KMAX];
+  __shared__ int m_key[NBMAX + KMAX];
+  __shared__ float old_fs[NBMAX];
+  __shared__ int old_fl[NBMAX], old_ff[NBMAX];
+  __shared__ int hist[NBMAX][TMAX];  // parents' token histories (ids < 2^31)
+  __shared__ int bph[NBMAX][TMAX];   // parents' slot tables
+  __shared__ int fst[NBMAX][TMAX];   // the item's finished rows before this step
+  __shared__ int last;
+  if (*a.done) return;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int nb = a.num_beams, K = 2 * nb;
+  const int L = *a.cur_len, P = a.begin_index;
+  const int V = (int)a.V;
+  const int r0 = b * nb;
+
+  // 1. candidates: row j's K processed log-probs + its running score; key = flat index j*V + v
+  const int n = nb * K;
+  for (int i = tid; i < n; i += BT) {
+    const int j = i / K;
+    cval[i] = a.cand_val[(int64_t)(r0 + j) * K + (i - j * K)] + a.run_scores[r0 + j];
+    ckey[i] = j * V + a.cand_idx[(int64_t)(r0 + j) * K + (i - j * K)];
+  }
+  for (int i = tid; i < nb; i += BT) {
+    old_fs[i] = a.fin_score[(int64_t)b * nb + i];
+    old_fl[i] = a.fin_len[(int64_t)b * nb + i];
+    old_ff[i] = a.fin_flag[(int64_t)b * nb + i];
+  }
+  // parents' histories (positions < L) and slot tables, before anything is rewritten
+  for (int i = tid; i < nb * L; i += BT) {
+    const int j = i / L, p = i - j * L;
+    hist[j][p] = (int)a.ids[(int64_t)(r0 + j) * a.ids_stride + p];
+    if (a.bp) bph[j][p] = a.bp[(int64_t)(r0 + j) * a.bp_stride + p];
+  }
+  __syncthreads();
+  // 2. top-K continuations (:3077-3129)
+  block_topk(cval, ckey, n, K, top, shf, shi);
+  const bool at_max = L + 1 >= a.max_length;
+  if (tid < K) {
+    const int i = top[tid];
+    t_lp[tid] = cval[i];
+    t_par[tid] = ckey[i] / V;
+    t_tok[tid] = ckey[i] - (ckey[i] / V) * V;
+    const int hit = at_max || t_tok[tid] == a.eos_id;  // MaxLength / EOS criteria on the new sequence
+    t_hit[tid] = hit;
+    t_run[tid] = t_lp[tid] + (hit ? 1.f : 0.f) * NEG;  // :3144
+  }
+  __syncthreads();
+  // 3. running beams for the next step (:3131-3151): top nb of t_run, key = candidate rank
+  if (tid < K) {
+    cval[tid] = t_run[tid];
+    ckey[tid] = tid;
+  }
+  __syncthreads();
+  block_topk(cval, ckey, K, nb, run_pos, shf, shi);
+  // 4. finished beams (:3153-3205)
+  if (tid == 0) {
+    int all_fin = 1;
+    for (int j = 0; j < nb; ++j) all_fin &= old_ff[j] != 0;
+    const float full = (all_fin && a.early_stopping == 1) ? 1.f : 0.f;
+    const float unsat0 = a.unsat[b] ? 0.f : 1.f;  // (~unsat) as f32
+    const float den = (float)pow((double)(L + 1 - P), (double)a.length_penalty);
+    for (int c = 0; c < K; ++c) {
+      const int did = t_hit[c] && c < nb;
+      float tl = t_lp[c] / den;
+      tl = tl + full * NEG;
+      tl = tl + unsat0 * NEG;
+      tl = tl + (did ? 0.f : 1.f) * NEG;
+      t_fin[c] = tl;
+    }
+    for (int j = 0; j < nb; ++j) {
+      m_val[j] = old_fs[j];
+      m_key[j] = j;
+    }
+    for (int c = 0; c < K; ++c) {
+      m_val[nb + c] = t_fin[c];
+      m_key[nb + c] = nb + c;
+    }
+  }
+  __syncthreads();
+  block_topk(m_val, m_key, nb + K, nb, fin_pos, shf, shi);
+  // 5. the new finished set: old entries come from the LDS copy, new ones are a candidate's parent
+  //    history + its token, fill (pad) beyond -- as the reference's static-shape sequences
+  const int Tf = (int)a.fin_stride;
+  for (int i = tid; i < nb * Tf; i += BT) {
+    const int j = i / Tf, p = i - j * Tf;
+    fst[j][p] = (int)a.fin_seq[((int64_t)b * nb + j) * Tf + p];
+  }
+  __shared__ int fin_src[NBMAX];
+  if (tid < nb) fin_src[tid] = fin_pos[tid];
+  __syncthreads();
+  for (int i = tid; i < nb * Tf; i += BT) {
+    const int s = i / Tf, p = i - s * Tf;
+    const int src = fin_src[s];
+    int v;
+    if (src < nb) {
+      v = fst[src][p];
+    } else {
+      const int c = src - nb;
+      v = p < L ? hist[t_par[c]][p] : (p == L ? t_tok[c] : a.fill_id);
+    }
+    a.fin_seq[((int64_t)b * nb + s) * Tf + p] = v;
+  }
+  if (tid < nb) {
+    const int src = fin_src[tid];
+    float fs;
+    int fl, ff;
+    if (src < nb) {
+      fs = old_fs[src];
+      fl = old_fl[src];
+      ff = old_ff[src];
+    } else {
+      fs = t_fin[src - nb];
+      fl = L + 1 - P;
+      ff = t_hit[src - nb] && (src - nb) < nb;
+    }
+    a.fin_score[(int64_t)b * nb + tid] = fs;
+    a.fin_len[(int64_t)b * nb + tid] = fl;
+    a.fin_flag[(int64_t)b * nb + tid] = ff;
+  }
+  // 6. running rows: parent history + new token, slot table of the parent + own slot at L
+  for (int i = tid; i < nb * (L + 1); i += BT) {
+    const int j = i / (L + 1), p = i - j * (L + 1);
+    const int c = run_pos[j];
+    a.ids[(int64_t)(r0 + j) * a.ids_stride + p] = p < L ? hist[t_par[c]][p] : (int64_t)t_tok[c];
+    if (a.bp) a.bp[(int64_t)(r0 + j) * a.bp_stride + p] = p < L ? bph[t_par[c]][p] : r0 + j;
+  }
+  if (tid < nb) a.run_scores[r0 + tid] = t_run[run_pos[tid]];
+  __syncthreads();
+  // 7. early-stop heuristic (:3008-3053) at cur_len + 1, and this item's loop-condition inputs
+  if (tid == 0) {
+    const int Ln = L + 1;
+    const int bhl = (a.early_stopping == 2 && a.length_penalty > 0.f) ? (a.max_length - P) : (Ln - P);
+    const float best_run = t_run[run_pos[0]] / (float)pow((double)bhl, (double)a.length_penalty);
+    float worst = INFINITY;
+    int all_fin = 1;
+    for (int j = 0; j < nb; ++j) {
+      worst = fminf(worst, a.fin_score[(int64_t)b * nb + j]);
+      all_fin &= a.fin_flag[(int64_t)b * nb + j] != 0;
+    }
+    int any_better = 0;
+    for (int j = 0; j < nb; ++j) {
+      const float wf = a.fin_flag[(int64_t)b * nb + j] ? worst : NEG;
+      any_better |= best_run > wf;
+    }
+    const int uns = a.unsat[b] && any_better;
+    a.unsat[b] = uns;
+    int all_hit = 1;
+    for (int c = 0; c < K; ++c) all_hit &= t_hit[c];
+    a.item_flags[3 * b] = uns;
+    a.item_flags[3 * b + 1] = all_fin;
+    a.item_flags[3 * b + 2] = all_hit;
+    __threadfence();
+    const int prev = atomicAdd(a.counter, 1);
+    last = prev == (int)a.B - 1;
+  }
+  __syncthreads();
+  // 8. the last item: _beam_search_has_unfinished_sequences over the batch, advance cur_len
+  if (last && tid == 0) {
+    __threadfence();
+    int improve = 0, all_fin = 1, all_hit = 1;
+    for (int i = 0; i < (int)a.B; ++i) {
+      improve |= __hip_atomic_load(a.item_flags + 3 * i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      all_fin &= __hip_atomic_load(a.item_flags + 3 * i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      all_hit &= __hip_atomic_load(a.item_flags + 3 * i + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int open = !(all_fin && a.early_stopping == 1);
+    const int go = improve && open && !all_hit;
+    *a.go = go;
+    if (!go) *a.done = 1;
+    *a.counter = 0;
+    *a.cur_len = L + 1;
+    __threadfence();
+  }
+}
+
+}  // namespace
+
+extern "C" int kw_beam_logprobs(const kw_beam_logprobs_args* a, kw_stream_t stream) {
+  if (!a || !a->logits || !a->suppress_mask || !a->ids || !a->cur_len || !a->cand_val || !a->cand_idx || !a->done ||
+      a->R <= 0 || a->V <= 0 || a->k < 1 || a->k > KMAX || (a->n_begin_suppress > 0 && !a->begin_suppress))
+    return kw_set_error_msg(KW_EINVAL, "kw_beam_logprobs: invalid arguments (k <= 16)");
+  hipLaunchKernelGGL(beam_logprobs_kernel, dim3((unsigned)a->R), dim3(ST), 0, (hipStream_t)stream, *a);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}
+
+extern "C" int kw_beam_select(const kw_beam_select_args* a, kw_stream_t stream) {
+  if (!a || a->B <= 0 || a->num_beams < 2 || a->num_beams > NBMAX || a->V <= 0 || !a->cand_val || !a->cand_idx ||
+      !a->ids || !a->run_scores || !a->fin_seq || !a->fin_score || !a->fin_len || !a->fin_flag ||
+      !a->unsat || !a->cur_len || !a->counter || !a->go || !a->done || !a->item_flags || a->fin_stride > TMAX ||
+      a->ids_stride < a->max_length || a->fin_stride < a->max_length || a->max_length > TMAX ||
+      (a->bp && a->bp_stride < a->max_length))
+    return kw_set_error_msg(KW_EINVAL, "kw_beam_select: invalid arguments (2 <= num_beams <= 8, max_length <= 512)");
+  hipLaunchKernelGGL(beam_select_kernel, dim3((unsigned)a->B), dim3(BT), 0, (hipStream_t)stream, *a);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}

@@ -11,68 +11,11 @@
 // of the four L2-resident passes (max, sum, timestamp log-sum-exp, argmax) instead of materialised.
 #include <math.h>
 
-#include "kw_common.h"
+#include "processors.h"
 
 namespace {
 
-constexpr int ST = 1024;
-
-struct RowState {
-  int L, begin, ts_begin, no_ts, eos;
-  int rt;          // return_timestamps
-  int last_ts, pen_ts, has_stamp, stamp_lo;  // stamp_lo: first allowed timestamp id
-  int first_step;
-  int max_init;    // -1 = none
-  int ban_text;
-};
-
-__device__ __forceinline__ float process(const RowState& st, const uint8_t* __restrict__ mask,
-                                         const int32_t* __restrict__ bsup, int nbsup, int v, float x) {
-  if (mask[v]) return -INFINITY;
-  if (st.first_step) {
-    for (int i = 0; i < nbsup; ++i)
-      if (bsup[i] == v) return -INFINITY;
-  }
-  if (st.rt) {
-    if (v == st.no_ts) return -INFINITY;
-    if (st.last_ts) {
-      if (st.pen_ts) {
-        if (v >= st.ts_begin) return -INFINITY;
-      } else {
-        if (v < st.eos) return -INFINITY;
-      }
-    }
-    if (st.has_stamp && v >= st.ts_begin && v < st.stamp_lo) return -INFINITY;
-    if (st.first_step) {
-      if (v < st.ts_begin) return -INFINITY;
-      if (st.max_init >= 0 && v > st.ts_begin + st.max_init) return -INFINITY;
-    }
-    if (st.ban_text && v < st.ts_begin) return -INFINITY;
-  }
-  return x;
-}
-
-__device__ float block_reduce_max(float v, float* sh) {
-  v = wave_max(v);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sh[w] = v;
-  __syncthreads();
-  float r = sh[0];
-  for (int i = 1; i < ST / 64; ++i) r = fmaxf(r, sh[i]);
-  __syncthreads();
-  return r;
-}
-
-__device__ float block_reduce_sum(float v, float* sh) {
-  v = wave_sum(v);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) sh[w] = v;
-  __syncthreads();
-  float r = 0.f;
-  for (int i = 0; i < ST / 64; ++i) r += sh[i];
-  __syncthreads();
-  return r;
-}
+using namespace kwp;
 
 __global__ __launch_bounds__(ST) void greedy_step_kernel(kw_sampler_args a) {
   __shared__ float shf[ST / 64];
@@ -85,76 +28,12 @@ __global__ __launch_bounds__(ST) void greedy_step_kernel(kw_sampler_args a) {
   const float* x = a.logits + (int64_t)b * a.V;
   const int V = (int)a.V;
 
-  // ---- history scan: finished flag and last timestamp position ---------------------------------
-  int fin = 0, last_stamp_pos = -1;
-  for (int p = a.begin_index + tid; p < L; p += ST) {
-    const int64_t t = ids[p];
-    if (t == a.eos_id) fin = 1;
-    if (t >= a.ts_begin && p > last_stamp_pos) last_stamp_pos = p;
-  }
-  fin = __syncthreads_or(fin);
-  {
-    int v = last_stamp_pos;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    if ((tid & 63) == 0) shi[tid >> 6][0] = v;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    int lp = shi[0][0];
-    for (int i = 1; i < ST / 64; ++i) lp = max(lp, shi[i][0]);
-    RowState st;
-    st.L = L; st.begin = a.begin_index; st.ts_begin = a.ts_begin; st.no_ts = a.no_ts_id; st.eos = a.eos_id;
-    st.rt = a.return_timestamps; st.max_init = a.max_initial_ts; st.ban_text = 0;
-    const int n = L - a.begin_index;
-    st.first_step = (L == a.begin_index);
-    st.last_ts = n >= 1 && ids[L - 1] >= a.ts_begin;
-    st.pen_ts = n < 2 || ids[L - 2] >= a.ts_begin;
-    st.has_stamp = lp >= 0;
-    if (st.has_stamp) {
-      const int last_stamp = (int)ids[lp];
-      st.stamp_lo = (st.last_ts && !st.pen_ts) ? last_stamp : last_stamp + 1;
-    } else {
-      st.stamp_lo = 0;
-    }
-    st_sh = st;
-  }
-  __syncthreads();
-  RowState st = st_sh;
-
+  // ---- history: finished flag and the WhisperTimeStamp row state --------------------------------
+  int fin = 0;
+  RowState st = row_state(ids, L, a.begin_index, a.ts_begin, a.no_ts_id, a.eos_id, a.return_timestamps,
+                          a.max_initial_ts, &fin, shi, &st_sh);
   // ---- timestamp probability-mass rule (logits_process.py:2040-2045) ---------------------------
-  if (st.rt) {
-    float m_all = -INFINITY, m_text = -INFINITY, m_ts = -INFINITY;
-    for (int v = tid; v < V; v += ST) {
-      const float s = process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, x[v]);
-      m_all = fmaxf(m_all, s);
-      if (v < st.ts_begin) m_text = fmaxf(m_text, s); else m_ts = fmaxf(m_ts, s);
-    }
-    m_all = block_reduce_max(m_all, shf);
-    m_text = block_reduce_max(m_text, shf);
-    m_ts = block_reduce_max(m_ts, shf);
-    float sum = 0.f;
-    for (int v = tid; v < V; v += ST) {
-      const float s = process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, x[v]);
-      sum += expf(s - m_all);
-    }
-    sum = block_reduce_sum(sum, shf);
-    const float lse = logf(sum);
-    // logprobs = (s - max) - log(sum); compare logsumexp(logprobs[ts:]) with max(logprobs[:ts])
-    const float lp_text_max = (m_text - m_all) - lse;
-    const float lp_ts_max = (m_ts - m_all) - lse;
-    float tsum = 0.f;
-    if (lp_ts_max > -INFINITY) {
-      for (int v = st.ts_begin + tid; v < V; v += ST) {
-        const float s = process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, x[v]);
-        const float lp = (s - m_all) - lse;
-        tsum += expf(lp - lp_ts_max);
-      }
-    }
-    tsum = block_reduce_sum(tsum, shf);
-    const float ts_lse = lp_ts_max > -INFINITY ? lp_ts_max + logf(tsum) : -INFINITY;
-    if (ts_lse > lp_text_max) st.ban_text = 1;
-  }
+  if (st.rt) timestamp_rule(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, V, [&](int v) { return x[v]; }, shf);
 
   // ---- argmax (first index on ties) -----------------------------------------------------------
   float best = -INFINITY;

@@ -63,6 +63,27 @@ class SamplerArgs(ctypes.Structure):
     ]
 
 
+class BeamLogprobsArgs(ctypes.Structure):
+    _fields_ = [
+        ("logits", c_vp), ("R", c_i64), ("V", c_i64),
+        ("suppress_mask", c_vp), ("begin_suppress", c_vp), ("n_begin_suppress", c_i32),
+        ("return_timestamps", c_i32), ("ts_begin", c_i32), ("no_ts_id", c_i32), ("eos_id", c_i32),
+        ("max_initial_ts", c_i32), ("ids", c_vp), ("ids_stride", c_i64), ("cur_len", c_vp),
+        ("begin_index", c_i32), ("k", c_i32), ("cand_val", c_vp), ("cand_idx", c_vp), ("done", c_vp),
+    ]
+
+
+class BeamSelectArgs(ctypes.Structure):
+    _fields_ = [
+        ("B", c_i64), ("num_beams", c_i32), ("V", c_i64), ("cand_val", c_vp), ("cand_idx", c_vp),
+        ("ids", c_vp), ("ids_stride", c_i64), ("bp", c_vp), ("bp_stride", c_i64), ("run_scores", c_vp),
+        ("fin_seq", c_vp), ("fin_stride", c_i64), ("fin_score", c_vp), ("fin_len", c_vp), ("fin_flag", c_vp),
+        ("unsat", c_vp), ("cur_len", c_vp), ("begin_index", c_i32), ("max_length", c_i32), ("eos_id", c_i32),
+        ("fill_id", c_i32), ("length_penalty", ctypes.c_float), ("early_stopping", c_i32),
+        ("counter", c_vp), ("go", c_vp), ("done", c_vp), ("item_flags", c_vp),
+    ]
+
+
 EXPORTS = {
     "kw_version": (ctypes.c_int, []),
     "kw_last_error": (ctypes.c_char_p, []),
@@ -77,12 +98,14 @@ EXPORTS = {
     "kw_attention": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kw_self_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
-                                         c_vp, c_vp, ctypes.c_size_t, c_vp]),
+                                         c_vp, c_i64, c_vp, c_vp, ctypes.c_size_t, c_vp]),
     "kw_self_attn_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64]),
     "kw_cross_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
                                           c_vp, ctypes.c_size_t, c_vp]),
     "kw_cross_attn_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64, c_i64]),
     "kw_greedy_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), c_vp]),
+    "kw_beam_logprobs": (ctypes.c_int, [ctypes.POINTER(BeamLogprobsArgs), c_vp]),
+    "kw_beam_select": (ctypes.c_int, [ctypes.POINTER(BeamSelectArgs), c_vp]),
 }
 
 _lib = None

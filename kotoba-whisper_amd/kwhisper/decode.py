@@ -23,21 +23,25 @@ T_MAX = 448
 
 
 class DecodeSession:
-    def __init__(self, eng, B: int, enc: torch.Tensor | None = None):
+    def __init__(self, eng, B: int, enc: torch.Tensor | None = None, beams: int = 1):
+        """B batch items decoded as R = B * beams running rows (item-major); cross K/V per item."""
         s = eng.shape
-        self.eng, self.B = eng, B
+        self.eng, self.B, self.nb = eng, B, beams
+        R = self.R = B * beams
         dev, dt = eng.device, eng.dtype
         d, H, Ld = s.d_model, eng.H, s.decoder_layers
         self.T = s.max_source_positions
         self.cross = torch.empty((2 * Ld, B, H, self.T, _HD), device=dev, dtype=dt)
-        self.kc = torch.zeros((Ld, B, H, T_MAX, _HD), device=dev, dtype=dt)
-        self.vc = torch.zeros((Ld, B, H, T_MAX, _HD), device=dev, dtype=dt)
-        self.ids = torch.zeros((B, T_MAX + 1), device=dev, dtype=torch.int64)
+        self.kc = torch.zeros((Ld, R, H, T_MAX, _HD), device=dev, dtype=dt)
+        self.vc = torch.zeros((Ld, R, H, T_MAX, _HD), device=dev, dtype=dt)
+        self.ids = torch.zeros((R, T_MAX + 1), device=dev, dtype=torch.int64)
+        # beam search: cache row holding position p of row r's history (beams share a prefix)
+        self.bp = torch.zeros((R, T_MAX), device=dev, dtype=torch.int32) if beams > 1 else None
         self.cur_len = torch.zeros((1,), device=dev, dtype=torch.int32)
-        self.unfinished = torch.ones((B,), device=dev, dtype=torch.int32)
+        self.unfinished = torch.ones((R,), device=dev, dtype=torch.int32)
         self.counter = torch.zeros((1,), device=dev, dtype=torch.int32)
         self.n_unfinished = torch.zeros((1,), device=dev, dtype=torch.int32)
-        self.logits = torch.empty((B, s.vocab_size), device=dev, dtype=torch.float32)
+        self.logits = torch.empty((R, s.vocab_size), device=dev, dtype=torch.float32)
         self._bufs = {}
         self._plans = {}
         # split-K seam scratch shared by every decode linear of a step (stream-ordered; zeroed once)
@@ -46,7 +50,7 @@ class DecodeSession:
             for n_, k_ in ((3 * d, d), (d, d), (s.decoder_ffn_dim, d), (d, s.decoder_ffn_dim), (s.vocab_size, d)):
                 ws = max(ws, ops.dec_linear_workspace_bytes(n_, k_))
         self.lin_ws = torch.zeros(((ws + 3) // 4,), device=dev, dtype=torch.float32) if ws else None
-        self.self_ws = torch.zeros((ops.self_attn_workspace_bytes(B, H, T_MAX) + 3) // 4, device=dev,
+        self.self_ws = torch.zeros((ops.self_attn_workspace_bytes(R, H, T_MAX) + 3) // 4, device=dev,
                                    dtype=torch.float32)
         self._graph = None
         self._graph_key = None
@@ -60,7 +64,7 @@ class DecodeSession:
     def _buffers(self, q: int):
         if q not in self._bufs:
             s, dev, dt = self.eng.shape, self.eng.device, self.eng.dtype
-            d, rows = s.d_model, self.B * q
+            d, rows = s.d_model, self.R * q
             self._bufs[q] = dict(
                 h=torch.empty((rows, d), device=dev, dtype=torch.float32),
                 x=torch.empty((rows, d), device=dev, dtype=dt),
@@ -69,7 +73,7 @@ class DecodeSession:
                 qx=torch.empty((rows, d), device=dev, dtype=dt),
                 ffn=torch.empty((rows, s.decoder_ffn_dim), device=dev, dtype=dt),
                 # cross-attention partials + arrival counters (must start zeroed; kernels leave them zeroed)
-                ws=torch.zeros((ops.cross_attn_workspace_bytes(self.B, q, self.eng.H, _HD, self.T) // 4 + 1,),
+                ws=torch.zeros((ops.cross_attn_workspace_bytes(self.B, q * self.nb, self.eng.H, _HD, self.T) // 4 + 1,),
                                device=dev, dtype=torch.float32),
             )
             if self.eng.packed:  # bf16 mirror of the residual stream (the LayerNorm-fused linears' operand)
@@ -86,7 +90,7 @@ class DecodeSession:
             return self._plans[q]
         eng, s = self.eng, self.eng.shape
         b = self._buffers(q)
-        d, H, B = s.d_model, eng.H, self.B
+        d, H, B = s.d_model, eng.H, self.R  # B: running rows
         rows = B * q
         scale = _HD ** -0.5
         eps = s.layer_norm_eps
@@ -141,7 +145,7 @@ class DecodeSession:
 
     def _run(self, seq):
         eng, s = self.eng, self.eng.shape
-        H, B = eng.H, self.B
+        H, B = eng.H, self.R
         for p in seq:
             if not isinstance(p, tuple):
                 p()
@@ -153,10 +157,12 @@ class DecodeSession:
                 ops.embed(self.ids, B, p[1], self.cur_len, eng.tok_emb, eng.dec_pos, p[2], p[3] if len(p) > 3 else None)
             elif k == "self":
                 _, q, qkv, li, out = p
-                ops.self_attn_step(qkv, B, q, H, _HD, self.kc[li], self.vc[li], T_MAX, self.cur_len, out, self.self_ws)
-            elif k == "cross":
+                ops.self_attn_step(qkv, B, q, H, _HD, self.kc[li], self.vc[li], T_MAX, self.cur_len, out, self.self_ws,
+                                   bp=self.bp if q == 1 else None)
+            elif k == "cross":  # rows b*nb*q + (beam*q + i) attend to item b's K/V
                 _, q, qx, li, out, ws = p
-                ops.cross_attn_step(qx, B, q, H, _HD, self.cross[2 * li], self.cross[2 * li + 1], self.T, out, ws)
+                ops.cross_attn_step(qx, self.B, q * self.nb, H, _HD, self.cross[2 * li], self.cross[2 * li + 1],
+                                    self.T, out, ws)
 
     # ------------------------------------------------------------------------------------------
     def forward_logits(self, prompt: torch.Tensor) -> torch.Tensor:
@@ -263,6 +269,93 @@ class DecodeSession:
         L_now = int(self.cur_len.item())
         ids = self.ids[:, :L_now].cpu().numpy()
         return _reference_length(ids, P, gen.eos_token_id, max_length)
+
+
+    def generate_beam(self, prompt: torch.Tensor, gen, *, num_beams: int, max_length: int, return_timestamps: bool,
+                      length_penalty: float = 1.0, early_stopping=False, check_every: int = 4, use_graph: bool = True):
+        """``GenerationMixin._beam_search`` (TF/generation/utils.py:3208-3527) on device, num_return_sequences 1.
+
+        ``prompt`` (B, P) per item.  Returns host int64 (B, P + generated) -- the best finished beam of each
+        item, pad-filled, cropped to the batch's longest -- as the reference returns ``sequences``."""
+        B, nb, R = self.B, self.nb, self.R
+        if nb != num_beams or nb < 2:
+            raise ValueError("session beam width mismatch")
+        P = prompt.shape[1]
+        if max_length > T_MAX:
+            raise ValueError(f"max_length {max_length} exceeds max_target_positions {T_MAX}")
+        dev = self.eng.device
+        V = self.eng.shape.vocab_size
+        fill = gen.pad_token_id if gen.pad_token_id is not None else gen.eos_token_id
+        self.ids.zero_()
+        self.ids[:, :P].copy_(prompt.to(dev).repeat_interleave(nb, 0))
+        self.cur_len.fill_(P)
+        self.bp.copy_(torch.arange(R, device=dev, dtype=torch.int32)[:, None].expand(R, T_MAX))
+        run = torch.zeros((B, nb), device=dev, dtype=torch.float32)
+        run[:, 1:] = -1.0e9
+        st = dict(
+            ids=self.ids, bp=self.bp, cur_len=self.cur_len, run_scores=run.view(-1),
+            fin_seq=torch.full((B, nb, max_length), fill, device=dev, dtype=torch.int64),
+            fin_score=torch.full((B, nb), -1.0e9, device=dev, dtype=torch.float32),
+            fin_len=torch.zeros((B, nb), device=dev, dtype=torch.int32),
+            fin_flag=torch.zeros((B, nb), device=dev, dtype=torch.int32),
+            unsat=torch.ones((B,), device=dev, dtype=torch.int32),
+            counter=torch.zeros((1,), device=dev, dtype=torch.int32),
+            go=torch.ones((1,), device=dev, dtype=torch.int32),
+            done=torch.zeros((1,), device=dev, dtype=torch.int32),
+            item_flags=torch.zeros((B, 3), device=dev, dtype=torch.int32),
+            cand_val=torch.empty((R, 2 * nb), device=dev, dtype=torch.float32),
+            cand_idx=torch.empty((R, 2 * nb), device=dev, dtype=torch.int32),
+        )
+        sup = torch.zeros((V,), dtype=torch.uint8)
+        if gen.suppress_tokens:
+            sup[torch.tensor(gen.suppress_tokens)] = 1
+        self._sup = sup.to(dev)
+        bsup = torch.tensor(gen.begin_suppress_tokens or [0], dtype=torch.int32, device=dev)
+        step = ops.BeamStepPlan(st, self.logits, self._sup, bsup if gen.begin_suppress_tokens else None,
+                                return_timestamps=return_timestamps, ts_begin=gen.timestamp_begin,
+                                no_ts_id=gen.no_timestamps_token_id, eos_id=gen.eos_token_id,
+                                max_initial_ts=gen.max_initial_timestamp_index, begin_index=P, max_length=max_length,
+                                fill_id=fill, length_penalty=length_penalty, early_stopping=early_stopping)
+        self._beam_state = st
+        self._run(self._step_plans(P))  # prefill on every running row (the reference expands x num_beams)
+        step()
+        step_seq = self._step_plans(1)
+
+        def one_step():
+            self._run(step_seq)
+            step()
+
+        graph = None
+        if use_graph:
+            graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.graph(graph, stream=side):
+                one_step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+        pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
+        events = []
+        n = 1
+        while n < max_length - P + 1:
+            if graph is not None:
+                graph.replay()
+            else:
+                one_step()
+            n += 1
+            slot = n % (check_every + 1)
+            pinned[slot: slot + 1].copy_(st["go"], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            events.append((ev, slot))
+            if len(events) > check_every:
+                e0, s0 = events.pop(0)
+                e0.synchronize()
+                if int(pinned[s0]) == 0:
+                    break
+        torch.cuda.synchronize(dev)
+        fin_len = st["fin_len"][:, 0].cpu().numpy()
+        out = st["fin_seq"][:, 0].cpu().numpy()
+        return out[:, : P + int(fin_len.max())]
 
 
 def _reference_length(ids: np.ndarray, P: int, eos: int, max_length: int) -> np.ndarray:

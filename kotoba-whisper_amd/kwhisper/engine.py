@@ -249,7 +249,7 @@ class WhisperEngine:
                      hs_seq=T, hs_heads=self.H, hs_head_dim=_HD)()
         return out
 
-    def new_session(self, B: int, enc: torch.Tensor | None = None) -> "DecodeSession":
+    def new_session(self, B: int, enc: torch.Tensor | None = None, beams: int = 1) -> "DecodeSession":
         from .decode import DecodeSession
 
-        return DecodeSession(self, B, enc)
+        return DecodeSession(self, B, enc, beams=beams)

@@ -13,6 +13,7 @@ TF/models/whisper/generation_whisper.py:383-968):
   * strip prompt / pad-count quirk / strip EOS                       :1042-1086
   * segments and right padding with ``pad_token_id``                 :1977-2074, :126-237
   * ``return_dict_in_generate`` (no timestamps): sequences incl. prompt  :916-934
+  * ``num_beams`` > 1: GenerationMixin._beam_search on device (TF/generation/utils.py:3208-3527)
 """
 from __future__ import annotations
 
@@ -33,7 +34,7 @@ _SUPPORTED = {
     "compression_ratio_threshold", "logprob_threshold", "no_speech_threshold", "return_token_timestamps",
     "output_scores", "output_logits", "time_precision", "time_precision_features", "num_segment_frames",
     "synced_gpus", "force_unique_generate_call", "prefix_allowed_tokens_fn", "prompt_condition_type",
-    "monitor_progress", "use_cache", "num_return_sequences",
+    "monitor_progress", "use_cache", "num_return_sequences", "length_penalty", "early_stopping",
 }
 
 
@@ -135,10 +136,11 @@ class KWhisperForConditionalGeneration:
         return cls.from_state_dict(shape, sd, dtype=torch_dtype, device=device, generation_config=gen)
 
     # ---- generate ---------------------------------------------------------------------------------
-    def _session(self, B):
-        if B not in self._sessions:
-            self._sessions[B] = self.engine.new_session(B)
-        return self._sessions[B]
+    def _session(self, B, beams=1):
+        key = (B, beams)
+        if key not in self._sessions:
+            self._sessions[key] = self.engine.new_session(B, beams=beams)
+        return self._sessions[key]
 
     def generate(self, input_features=None, generation_config=None, logits_processor=None, stopping_criteria=None,
                  return_timestamps=None, task=None, language=None, is_multilingual=None, attention_mask=None,
@@ -163,8 +165,10 @@ class KWhisperForConditionalGeneration:
         if isinstance(gen, dict):
             gen = GenerationConstants(**gen)
         num_beams = kwargs.get("num_beams", gen.num_beams or 1)
-        if num_beams != 1:
-            raise NotImplementedError("num_beams > 1 is not implemented on device yet (SURVEY §8f row 2)")
+        if num_beams > 8:
+            raise NotImplementedError("num_beams > 8 is not supported by the device beam search")
+        length_penalty = kwargs.get("length_penalty", getattr(gen, "length_penalty", 1.0))
+        early_stopping = kwargs.get("early_stopping", getattr(gen, "early_stopping", False))
         max_new_tokens = kwargs.get("max_new_tokens")
         max_length = kwargs.get("max_length", gen.max_length)
         s = self.engine.shape
@@ -249,9 +253,15 @@ class KWhisperForConditionalGeneration:
                 eff_max = max_length
             else:
                 eff_max = P + max_new_tokens
-            sess = self._session(cur)
+            sess = self._session(cur, num_beams)
             sess.set_encoder_output(enc)
-            ids = sess.generate(torch.from_numpy(prompt), gen, max_length=eff_max, return_timestamps=return_timestamps)
+            if num_beams > 1:
+                ids = sess.generate_beam(torch.from_numpy(prompt), gen, num_beams=num_beams, max_length=eff_max,
+                                         return_timestamps=return_timestamps, length_penalty=length_penalty,
+                                         early_stopping=early_stopping)
+            else:
+                ids = sess.generate(torch.from_numpy(prompt), gen, max_length=eff_max,
+                                    return_timestamps=return_timestamps)
             passes += 1
             last_ids = ids
             pad, eos = gen.pad_token_id, gen.eos_token_id

@@ -229,12 +229,14 @@ def self_attn_workspace_bytes(B, H, t_max) -> int:
     return int(_lib().kw_self_attn_workspace(B, H, t_max))
 
 
-def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out, workspace=None):
-    """Static-cache self-attention; q_len == 1 needs a zero-filled ``workspace`` (self_attn_workspace_bytes)."""
-    _cuda(qkv, k_cache, v_cache, cur_len, out, workspace)
+def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out, workspace=None, bp=None):
+    """Static-cache self-attention; q_len == 1 needs a zero-filled ``workspace`` (self_attn_workspace_bytes);
+    ``bp``: beam-search slot table [B][>= t_max] int32 (q_len == 1)."""
+    _cuda(qkv, k_cache, v_cache, cur_len, out, workspace, bp)
     nb = workspace.numel() * workspace.element_size() if workspace is not None else 0
     L.check(_lib().kw_self_attn_step(_dt(qkv), _p(qkv), B, q_len, H, hd, _p(k_cache), _p(v_cache), t_max,
-                                     _p(cur_len), _p(out), _p(workspace), nb, _s()), "kw_self_attn_step")
+                                     _p(cur_len), _p(bp), bp.stride(0) if bp is not None else 0, _p(out),
+                                     _p(workspace), nb, _s()), "kw_self_attn_step")
 
 
 def cross_attn_workspace_bytes(B, q_len, H, hd, S) -> int:
@@ -278,3 +280,48 @@ class SamplerPlan:
 
     def __call__(self):
         L.check(_lib().kw_greedy_step(self._ref, _s()), "kw_greedy_step")
+
+
+class BeamStepPlan:
+    """Pre-built ``kw_beam_logprobs`` + ``kw_beam_select`` calls for one beam-search step."""
+
+    def __init__(self, st, logits, suppress_mask, begin_suppress, *, return_timestamps, ts_begin, no_ts_id, eos_id,
+                 max_initial_ts, begin_index, max_length, fill_id, length_penalty, early_stopping):
+        """``st``: a dict of the device state tensors (see DecodeSession.generate_beam)."""
+        self._keep = (st, logits, suppress_mask, begin_suppress)
+        R, V = logits.shape
+        B, nb = st["fin_score"].shape
+        a = L.BeamLogprobsArgs()
+        a.logits, a.R, a.V = logits.data_ptr(), R, V
+        a.suppress_mask = suppress_mask.data_ptr()
+        a.begin_suppress = begin_suppress.data_ptr() if begin_suppress is not None else None
+        a.n_begin_suppress = begin_suppress.numel() if begin_suppress is not None else 0
+        a.return_timestamps = int(bool(return_timestamps))
+        a.ts_begin, a.no_ts_id, a.eos_id = ts_begin, no_ts_id, eos_id
+        a.max_initial_ts = -1 if max_initial_ts is None else max_initial_ts
+        a.ids, a.ids_stride = st["ids"].data_ptr(), st["ids"].stride(0)
+        a.cur_len = st["cur_len"].data_ptr()
+        a.begin_index = begin_index
+        a.k = 2 * nb
+        a.cand_val, a.cand_idx, a.done = st["cand_val"].data_ptr(), st["cand_idx"].data_ptr(), st["done"].data_ptr()
+        b = L.BeamSelectArgs()
+        b.B, b.num_beams, b.V = B, nb, V
+        b.cand_val, b.cand_idx = a.cand_val, a.cand_idx
+        b.ids, b.ids_stride = a.ids, a.ids_stride
+        b.bp = st["bp"].data_ptr() if st.get("bp") is not None else None
+        b.bp_stride = st["bp"].stride(0) if st.get("bp") is not None else 0
+        b.run_scores = st["run_scores"].data_ptr()
+        b.fin_seq, b.fin_stride = st["fin_seq"].data_ptr(), st["fin_seq"].shape[-1]
+        b.fin_score, b.fin_len, b.fin_flag = st["fin_score"].data_ptr(), st["fin_len"].data_ptr(), st["fin_flag"].data_ptr()
+        b.unsat, b.cur_len = st["unsat"].data_ptr(), a.cur_len
+        b.begin_index, b.max_length, b.eos_id, b.fill_id = begin_index, max_length, eos_id, fill_id
+        b.length_penalty = float(length_penalty)
+        b.early_stopping = 2 if early_stopping == "never" else int(bool(early_stopping))
+        b.counter, b.go, b.done = st["counter"].data_ptr(), st["go"].data_ptr(), a.done
+        b.item_flags = st["item_flags"].data_ptr()
+        self.a, self.b = a, b
+        self._ra, self._rb = ctypes.byref(a), ctypes.byref(b)
+
+    def __call__(self):
+        L.check(_lib().kw_beam_logprobs(self._ra, _s()), "kw_beam_logprobs")
+        L.check(_lib().kw_beam_select(self._rb, _s()), "kw_beam_select")

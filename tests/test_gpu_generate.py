@@ -15,7 +15,7 @@ pytestmark = pytest.mark.gpu
 from kwhisper.config import KOTOBA_V2, LARGE_V3, TINY, generation_constants  # noqa: E402
 from kwhisper.synthetic import synthetic_state_dict  # noqa: E402
 
-from _util import TINY_MODES, oracle_features  # noqa: E402
+from _util import BEAM_MODES, TINY_MODES, oracle_features  # noqa: E402
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -64,6 +64,30 @@ def test_tiny_fp32_generate_bitexact(gold, tiny32, mode):
         np.testing.assert_array_equal(toks.cpu().numpy(), g[f"{mode}_tokens"])
     finally:
         model.generation_config = generation_constants(TINY)
+
+
+@pytest.mark.parametrize("mode", sorted(BEAM_MODES))
+def test_tiny_fp32_beam_bitexact(gold, tiny32, mode):
+    """Device beam search (kw_beam_logprobs + kw_beam_select, slot-table self-attention) against HF beam
+    search: EOS finishing, length penalty, early_stopping True / "never", timestamps; bit-exact tokens."""
+    g = gold("tiny_beam_fp32")
+    kw, eos = BEAM_MODES[mode]
+    gen = generation_constants(TINY)
+    if eos is not None:
+        gen.eos_token_id = eos
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    toks = tiny32.generate(feats, generation_config=gen, **kw)
+    np.testing.assert_array_equal(toks.cpu().numpy(), g[f"{mode}_tokens"])
+
+
+def test_tiny_bf16_beam_runs(gold, tiny16):
+    """bf16 engine: beam search with timestamps runs end to end (graph-replayed) with valid ids."""
+    g = gold("tiny_beam_fp32")
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    toks = tiny16.generate(feats, language="ja", task="transcribe", return_timestamps=True, num_beams=5,
+                           max_length=40).cpu().numpy()
+    assert toks.shape[0] == 4 and 0 < toks.shape[1] <= 40
+    assert toks.min() >= 0 and toks.max() < TINY.vocab_size
 
 
 def test_tiny_fp32_logits(gold, tiny32):
