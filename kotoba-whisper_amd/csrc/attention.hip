@@ -126,9 +126,20 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
         mx = fmaxf(mx, st[i][r]);
       }
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f((m_run - m_new) * LOG2E);
-    const float mneg = -m_new * LOG2E;
+    // deferred rescale: the exponent reference m_run only moves when a score exceeds it by more than
+    // 8 (p <= e^8, exact in f32 and in bf16's range); most tiles skip the O / l rescale entirely
+    const bool bump = mx > m_run + 8.0f;
+    if (__builtin_amdgcn_ballot_w64(bump)) {
+      const float m_new = bump ? mx : m_run;
+      const float alpha = bump ? exp2f((m_run - m_new) * LOG2E) : 1.0f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+      l_run *= alpha;
+      m_run = m_new;
+    }
+    const float mneg = -m_run * LOG2E;
     float rs = 0.f;
     bf16x8 pf[2][2];
 #pragma unroll
@@ -142,12 +153,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
           pf[i][s][e] = (__bf16)p;
         }
     rs += __shfl_xor(rs, 32, 64);
-    l_run = l_run * alpha + rs;
-    m_run = m_new;
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+    l_run += rs;
 
     // O^T += V^T P^T ; A operand via ds_read_b64_tr_b16 from the row-major V tile
     const int li = lane & 15, qq = li >> 2, pp = li & 3, grp = (lane >> 4) & 1;

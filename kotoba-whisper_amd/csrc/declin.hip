@@ -249,7 +249,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
             p.hb[(int64_t)m * p.ldh + n] = f2bf(v);
           }
         } else {
-          if (p.gelu) v = gelu_erf(v);
+          if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
           if (n < p.scale_cols) v *= p.scale;
           if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
         }

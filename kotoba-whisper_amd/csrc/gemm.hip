@@ -330,7 +330,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
         const float* ra = p.row_add ? p.row_add + (int64_t)(m % p.row_add_period) * p.N + n : nullptr;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if (p.gelu) v[e] = gelu_erf(v[e]);
+          if (p.gelu) v[e] = sizeof(TC) == 2 ? gelu_bf16out(v[e]) : gelu_erf(v[e]);
           v[e] *= cs[e];
           if (ra) v[e] += ra[e];
         }

@@ -38,6 +38,16 @@ __device__ __forceinline__ float gelu_erf(float x) {
   return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
 }
 
+__device__ __forceinline__ float gelu_bf16out(float x) {
+  // GELU for a bf16 result: erf by Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7, far below bf16's
+  // 2^-9 rounding) -- one rcp + one exp instead of the erff library call; f32 results use gelu_erf
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
+  const float e = 1.0f - poly * __expf(-z * z);
+  return 0.5f * x * (1.0f + copysignf(e, x));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -26,6 +26,7 @@ def main():
     res = {"tile": os.environ.get("KW_GEMM_TILE", "default")}
     x = torch.randn(M, F, device=dev).bfloat16()
     for name, N, K, epi in [("qkv_headsplit", 3 * d, d, L.KW_EPI_HEADSPLIT), ("o_resid", d, d, L.KW_EPI_RESID),
+                            ("o_store_bf16", d, d, L.KW_EPI_STORE), ("fc2_store_bf16", d, F, L.KW_EPI_STORE),
                             ("fc1_gelu", F, d, L.KW_EPI_STORE), ("fc2_resid", d, F, L.KW_EPI_RESID),
                             ("cross_kv_headsplit", 2 * 32 * d, d, L.KW_EPI_HEADSPLIT)]:
         W = (torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()
