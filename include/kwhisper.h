@@ -121,9 +121,11 @@ int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed, kw_stream_
 size_t kw_packed_weight_bytes(int64_t N, int64_t K);
 
 /* LayerNorm (eps) over the last dim of x [rows][dim] f32 -> y [rows][dim] (y_dtype);
- * TF modeling_whisper.py:371,377,434,443,446,642,790. dim % 4 == 0, dim <= 2048. */
-int kw_layernorm(const float* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
-                 float eps, void* y, int y_dtype, kw_stream_t stream);
+ * TF modeling_whisper.py:371,377,434,443,446,642,790. dim % 4 == 0, dim <= 2048.  delta (bf16
+ * [rows][dim] or NULL): the producing linear's output, added to x in place first (the residual add
+ * of :398,407 fused in front of the next LayerNorm). */
+int kw_layernorm(float* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
+                 float eps, void* y, int y_dtype, const void* delta, kw_stream_t stream);
 
 /* Encoder self-attention softmax(Q K^T) V (q pre-scaled; TF sdpa_attention.py:79-166, non-causal).
  * qkv: [3][B][H][T][hd] (dtype), out: [B][T][H*hd] (dtype). hd == 64. */

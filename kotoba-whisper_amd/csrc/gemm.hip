@@ -145,8 +145,8 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmP p) {
 // tile t in slot 2t) and retires it at the end of slot 2t+3.  Both are read from slot 2t+2 / 2t+4 on.
 //
 // Epilogue: each wave stages its 128x64 f32 results through a private 17 KB LDS region (64 rows at a
-// time, 272-B padded rows: conflict-free b32 writes) and stores 16-B (f32) / 8-B (bf16) row pieces,
-// so every wave store instruction covers 4 rows x 64 contiguous columns.
+// time, 272-B padded rows: conflict-free b32 writes) and stores 16-B row pieces (4 f32 / 8 bf16), so
+// every wave store instruction covers 4 (f32) or 8 (bf16) rows x 64 contiguous columns.
 // ------------------------------------------------------------------------------------------------
 constexpr int PB = 256, PK = 64;
 constexpr int P_OP = PB * PK * 2;  // 32 KB: one operand image of one K-tile
@@ -279,13 +279,17 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
     }
   }
 
-  // epilogue (LDS is free: every wave passed the last barrier, every glds retired)
+  // epilogue (LDS is free: every wave passed the last barrier, every glds retired).  bf16 output:
+  // 8 columns (16 B) per lane, 8 rows per store instruction; f32 (RESID / f32 store): 4 columns, 4 rows.
+  constexpr int VEC = (EPI != KW_EPI_RESID && sizeof(TC) == 2) ? 8 : 4;
+  constexpr int LPR = 64 / VEC;                  // lanes per 64-column row
+  constexpr int RPI = 64 / LPR;                  // rows per store instruction
   float* ep = reinterpret_cast<float*>(smem + wave * P_EPI);
-  const int cq = lane & 15;                      // this lane's 4-column group within the wave's 64 columns
-  const int n = n0 + wq * 64 + 4 * cq;           // first of its 4 columns
-  float cb[4], cs[4];
+  const int cq = lane % LPR;                     // this lane's VEC-column group within the wave's 64 columns
+  const int n = n0 + wq * 64 + VEC * cq;         // first of its VEC columns
+  float cb[VEC], cs[VEC];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
+  for (int e = 0; e < VEC; ++e) {
     cb[e] = p.bias ? p.bias[n + e] : 0.f;
     cs[e] = n + e < p.scale_cols ? p.scale : 1.f;
   }
@@ -307,12 +311,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) ep[(16 * ii + 4 * (lane >> 4) + r) * 68 + 16 * j + (lane & 15)] = acc[4 * half + ii][j][r];
 #pragma unroll 4
-    for (int q = 0; q < 16; ++q) {
-      const int rr = 4 * q + (lane >> 4);
+    for (int q = 0; q < 64 / RPI; ++q) {
+      const int rr = RPI * q + lane / LPR;
       const int m = m0 + grp * 128 + 64 * half + rr;
-      const float4 v4 = *reinterpret_cast<const float4*>(ep + rr * 68 + 4 * cq);
+      float v[VEC];
+#pragma unroll
+      for (int e = 0; e < VEC; e += 4) {
+        const float4 v4 = *reinterpret_cast<const float4*>(ep + rr * 68 + VEC * cq + e);
+        v[e] = v4.x + cb[e]; v[e + 1] = v4.y + cb[e + 1]; v[e + 2] = v4.z + cb[e + 2]; v[e + 3] = v4.w + cb[e + 3];
+      }
       if (m >= p.M) continue;
-      float v[4] = {v4.x + cb[0], v4.y + cb[1], v4.z + cb[2], v4.w + cb[3]};
       int64_t off;
       if constexpr (EPI == KW_EPI_HEADSPLIT) {
         const int bb = m / p.hs_seq, tt = m - bb * p.hs_seq;
@@ -329,7 +337,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
       } else {
         const float* ra = p.row_add ? p.row_add + (int64_t)(m % p.row_add_period) * p.N + n : nullptr;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e = 0; e < VEC; ++e) {
           if (p.gelu) v[e] = sizeof(TC) == 2 ? gelu_bf16out(v[e]) : gelu_erf(v[e]);
           v[e] *= cs[e];
           if (ra) v[e] += ra[e];
@@ -337,9 +345,12 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
         if constexpr (sizeof(TC) == 4) {
           *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
         } else {
-          ushort4 o;
-          o.x = f2bf(v[0]); o.y = f2bf(v[1]); o.z = f2bf(v[2]); o.w = f2bf(v[3]);
-          *reinterpret_cast<ushort4*>(reinterpret_cast<bf16_t*>(p.C) + off) = o;
+          uint4 o;
+          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+          o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+          o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = o;
         }
       }
     }
@@ -435,9 +446,10 @@ bool use256(const kw_gemm_args* a) {
     const char* e = getenv("KW_GEMM_TILE");
     forced = (e && atoi(e) == 128) ? 1 : 0;
   }
-  // 4-column vector epilogue: ldc, batch strides, head_dim and the C base 16-B aligned (f32) / 8-B (bf16)
-  const bool aligned = a->ldc % 4 == 0 && a->c_batch_stride % 4 == 0 && (a->hs_head_dim <= 0 || a->hs_head_dim % 4 == 0) &&
-                       ((uintptr_t)a->C % (a->c_dtype == KW_DT_F32 ? 16 : 8)) == 0;
+  // vector epilogue: ldc, batch strides, head_dim in whole 16-B pieces, the C base 16-B aligned
+  const int vec = (a->c_dtype == KW_DT_F32) ? 4 : 8;  // 16-B pieces: 4 f32 / 8 bf16 columns
+  const bool aligned = a->ldc % vec == 0 && a->c_batch_stride % vec == 0 &&
+                       (a->hs_head_dim <= 0 || a->hs_head_dim % vec == 0) && ((uintptr_t)a->C % 16) == 0;
   return !forced && aligned && a->N % PB == 0 && a->M >= 4 * PB;
 }
 

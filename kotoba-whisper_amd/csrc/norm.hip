@@ -7,14 +7,17 @@ namespace {
 // TF/models/whisper/modeling_whisper.py:371,377,434,443,446,642,790 (nn.LayerNorm, eps 1e-5).
 constexpr int LN_MAXV = 8;  // float4 per lane -> dim <= 64*4*8 = 2048
 
+// With ``delta`` (bf16, optional) the residual add of the producing linear is fused in front:
+// x += delta is written back (the f32 residual stream), then normalised (modeling_whisper.py:398,407).
 template <typename TOut>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, int64_t rows, int dim,
+__global__ __launch_bounds__(256) void layernorm_kernel(float* __restrict__ x, int64_t rows, int dim,
                                                         const float* __restrict__ g, const float* __restrict__ bta,
-                                                        float eps, TOut* __restrict__ y) {
+                                                        float eps, TOut* __restrict__ y, const bf16_t* __restrict__ delta) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const float4* xr = reinterpret_cast<const float4*>(x + row * dim);
+  float4* xr = reinterpret_cast<float4*>(x + row * dim);
+  const ushort4* dr = delta ? reinterpret_cast<const ushort4*>(delta + row * dim) : nullptr;
   const int nv = dim >> 2;
   float4 v[LN_MAXV];
   float s = 0.f;
@@ -23,6 +26,14 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
     const int c = i * 64 + lane;
     if (c < nv) {
       v[i] = xr[c];
+      if (dr) {
+        const ushort4 dd = dr[c];
+        v[i].x += bf2f(dd.x);
+        v[i].y += bf2f(dd.y);
+        v[i].z += bf2f(dd.z);
+        v[i].w += bf2f(dd.w);
+        xr[c] = v[i];
+      }
       s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
     } else {
       v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -103,17 +114,19 @@ __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ 
 
 }  // namespace
 
-extern "C" int kw_layernorm(const float* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
-                            float eps, void* y, int y_dtype, kw_stream_t stream) {
+extern "C" int kw_layernorm(float* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
+                            float eps, void* y, int y_dtype, const void* delta, kw_stream_t stream) {
   if (!x || !gamma || !beta || !y || rows < 0 || dim <= 0 || dim % 4 != 0 || dim > 64 * 4 * LN_MAXV)
     return kw_set_error_msg(KW_EINVAL, "kw_layernorm: invalid arguments (dim % 4 == 0, dim <= 2048)");
   if (rows == 0) return KW_OK;
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)((rows + 3) / 4));
   if (y_dtype == KW_DT_F32)
-    hipLaunchKernelGGL(layernorm_kernel<float>, grid, dim3(256), 0, s, x, rows, (int)dim, gamma, beta, eps, (float*)y);
+    hipLaunchKernelGGL(layernorm_kernel<float>, grid, dim3(256), 0, s, x, rows, (int)dim, gamma, beta, eps, (float*)y,
+                       (const bf16_t*)delta);
   else
-    hipLaunchKernelGGL(layernorm_kernel<bf16_t>, grid, dim3(256), 0, s, x, rows, (int)dim, gamma, beta, eps, (bf16_t*)y);
+    hipLaunchKernelGGL(layernorm_kernel<bf16_t>, grid, dim3(256), 0, s, x, rows, (int)dim, gamma, beta, eps, (bf16_t*)y,
+                       (const bf16_t*)delta);
   KW_CHECK_LAUNCH();
   return KW_OK;
 }

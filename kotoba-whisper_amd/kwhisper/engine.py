@@ -44,6 +44,9 @@ class _EncoderBuffers:
         self.attn = torch.empty((B * T, d), device=dev, dtype=dt)
         self.ffn = torch.empty((B * T, s.encoder_ffn_dim), device=dev, dtype=dt)
         self.out = torch.empty((B * T, d), device=dev, dtype=dt)
+        # bf16 path: out-proj / fc2 store their output here and the next LayerNorm adds it into h
+        # (a bf16 store is cheaper than the f32 read-modify-write of a residual epilogue)
+        self.delta = torch.empty((B * T, d), device=dev, dtype=dt) if dt == torch.bfloat16 else None
         self.plans = eng._encoder_plans(self)
 
 
@@ -190,18 +193,26 @@ class WhisperEngine:
                                   lda=2 * d, a_rows_per_batch=T, a_batch_stride=(F + 2) * d,
                                   gelu=True, row_add=self.enc_pos, row_add_period=T))
         scale = _HD ** -0.5
+        dl, pending = bf.delta, None  # pending: the delta the next LayerNorm must add into h first
         for lay in self.enc_layers:
-            plans.append(("ln", bf.h, lay["ln1_g"], lay["ln1_b"], bf.x))
+            plans.append(("ln", bf.h, lay["ln1_g"], lay["ln1_b"], bf.x, pending))
             plans.append(ops.GemmPlan(bf.x, lay["qkv_w"], bf.qkv, M, 3 * d, d, bias=lay["qkv_b"],
                                       epilogue=L.KW_EPI_HEADSPLIT, scale=scale, scale_cols=d,
                                       hs_seq=T, hs_heads=self.H, hs_head_dim=_HD))
             plans.append(("attn", bf.qkv, bf.attn))
-            plans.append(ops.GemmPlan(bf.attn, lay["o_w"], bf.h, M, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID))
-            plans.append(("ln", bf.h, lay["ln2_g"], lay["ln2_b"], bf.x))
+            if dl is None:
+                plans.append(ops.GemmPlan(bf.attn, lay["o_w"], bf.h, M, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID))
+            else:
+                plans.append(ops.GemmPlan(bf.attn, lay["o_w"], dl, M, d, d, bias=lay["o_b"]))
+            plans.append(("ln", bf.h, lay["ln2_g"], lay["ln2_b"], bf.x, dl))
             plans.append(ops.GemmPlan(bf.x, lay["fc1_w"], bf.ffn, M, s.encoder_ffn_dim, d, bias=lay["fc1_b"], gelu=True))
-            plans.append(ops.GemmPlan(bf.ffn, lay["fc2_w"], bf.h, M, d, s.encoder_ffn_dim, bias=lay["fc2_b"],
-                                      epilogue=L.KW_EPI_RESID))
-        plans.append(("ln", bf.h, self.enc_ln_g, self.enc_ln_b, bf.out))
+            if dl is None:
+                plans.append(ops.GemmPlan(bf.ffn, lay["fc2_w"], bf.h, M, d, s.encoder_ffn_dim, bias=lay["fc2_b"],
+                                          epilogue=L.KW_EPI_RESID))
+            else:
+                plans.append(ops.GemmPlan(bf.ffn, lay["fc2_w"], dl, M, d, s.encoder_ffn_dim, bias=lay["fc2_b"]))
+            pending = dl
+        plans.append(("ln", bf.h, self.enc_ln_g, self.enc_ln_b, bf.out, pending))
         return plans
 
     def encoder_buffers(self, B: int) -> _EncoderBuffers:
@@ -230,7 +241,7 @@ class WhisperEngine:
         for p in bf.plans:
             if isinstance(p, tuple):
                 if p[0] == "ln":
-                    ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4])
+                    ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4], delta=p[5])
                 else:
                     ops.attention(p[1], B, self.H, T, _HD, p[2])
             else:

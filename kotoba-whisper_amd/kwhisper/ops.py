@@ -71,13 +71,18 @@ def mel_to_time_major(mel: torch.Tensor, c_pad: int, dtype: torch.dtype, out: to
     return out
 
 
-def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor):
-    _cuda(x, gamma, beta, out)
+def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor,
+              delta: torch.Tensor | None = None):
+    """out = LayerNorm(x) (x f32); with ``delta`` (bf16, x's shape) x += delta first, in place."""
+    _cuda(x, gamma, beta, out, delta)
     if x.dtype != torch.float32 or not x.is_contiguous():
         raise ValueError("layernorm input must be contiguous float32")
+    if delta is not None and (delta.dtype != torch.bfloat16 or delta.numel() != x.numel() or not delta.is_contiguous()):
+        raise ValueError("layernorm delta must be a contiguous bf16 tensor of x's size")
     dim = x.shape[-1]
     rows = x.numel() // dim
-    L.check(_lib().kw_layernorm(_p(x), rows, dim, _p(gamma), _p(beta), eps, _p(out), _dt(out), _s()), "kw_layernorm")
+    L.check(_lib().kw_layernorm(_p(x), rows, dim, _p(gamma), _p(beta), eps, _p(out), _dt(out), _p(delta), _s()),
+            "kw_layernorm")
     return out
 
 

@@ -70,6 +70,6 @@ def test_struct_layout_matches_c(cname, pyname):
 
 def test_errors_are_returned_not_thrown(lib):
     """Invalid arguments come back as KW_EINVAL with a message (no HIP call is made)."""
-    rc = lib.kw_layernorm(None, 1, 7, None, None, 1e-5, None, 0, None)
+    rc = lib.kw_layernorm(None, 1, 7, None, None, 1e-5, None, 0, None, None)
     assert rc == 1
     assert b"kw_layernorm" in lib.kw_last_error()

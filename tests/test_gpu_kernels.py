@@ -220,6 +220,21 @@ def test_layernorm(rows, dim, out_dtype):
     torch.testing.assert_close(y.float(), ref, atol=tol * 4, rtol=tol)
 
 
+@pytest.mark.parametrize("rows,dim", [(3, 384), (48000, 1280)])
+def test_layernorm_residual_delta(rows, dim):
+    """x += delta (bf16, written back) then LayerNorm: the encoder's fused residual add."""
+    x = torch.randn(rows, dim, device="cuda") * 3 + 1
+    delta = (torch.randn(rows, dim, device="cuda") * 2).to(torch.bfloat16)
+    g = torch.randn(dim, device="cuda")
+    b = torch.randn(dim, device="cuda")
+    want_h = x + delta.float()
+    y = torch.empty(rows, dim, device="cuda", dtype=torch.bfloat16)
+    ops.layernorm(x, g, b, 1e-5, y, delta=delta)
+    torch.testing.assert_close(x, want_h, atol=0, rtol=0)
+    ref = torch.nn.functional.layer_norm(want_h.double(), (dim,), g.double(), b.double(), 1e-5).float()
+    torch.testing.assert_close(y.float(), ref, atol=8e-2, rtol=2e-2)
+
+
 # ---------------------------------------------------------------- attention
 def _ref_attn(qkv, B, H, T, hd):
     q, k, v = qkv.float().view(3, B, H, T, hd)

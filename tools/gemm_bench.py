@@ -53,7 +53,35 @@ def main():
         e1.synchronize()
         us = e0.elapsed_time(e1) * 1e3 / reps
         res[name] = {"us": round(us, 1), "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
+        # hipBLASLt on the same shape (plain GEMM, bf16 out, no epilogue) for reference
+        if N <= 10000:
+            torch.matmul(A, W.t())
+            e0.record()
+            for _ in range(reps):
+                torch.matmul(A, W.t())
+            e1.record()
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / reps
+            res[name + "_hipblaslt"] = {"us": round(us, 1), "TFLOPs": round(2 * M * N * K / us / 1e6, 1)}
         del W, C
+    # encoder self-attention: ours vs torch SDPA (flash/CK on ROCm)
+    qkv = torch.randn(3, B, H, T, 64, device=dev).bfloat16() * 0.5
+    out = torch.empty(M, d, device=dev, dtype=torch.bfloat16)
+    flops = 4 * B * H * T * T * 64
+    for name, fn in [("attn", lambda: ops.attention(qkv, B, H, T, 64, out)),
+                     ("attn_sdpa", lambda: torch.nn.functional.scaled_dot_product_attention(qkv[0], qkv[1], qkv[2]))]:
+        try:
+            fn()
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(10):
+                fn()
+            e1.record()
+            e1.synchronize()
+            us = e0.elapsed_time(e1) * 1e3 / 10
+            res[name] = {"us": round(us, 1), "TFLOPs": round(flops / us / 1e6, 1)}
+        except Exception as e:  # noqa: BLE001
+            res[name] = str(e)[:100]
     print(json.dumps(res))
 
 
