@@ -16,6 +16,11 @@
 
 #include "gemm_common.h"
 
+// development hook (tools/lab/gemm_lab.hip defines it to record s_memtime stamps); no-op here
+#ifndef KW_GEMM_STAMP
+#define KW_GEMM_STAMP(slot)
+#endif
+
 namespace {
 using namespace kwg;
 
@@ -149,11 +154,26 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmP p) {
 // every wave store instruction covers 4 (f32) or 8 (bf16) rows x 64 contiguous columns.
 // ------------------------------------------------------------------------------------------------
 constexpr int PB = 256, PK = 64;
-constexpr int P_OP = PB * PK * 2;  // 32 KB: one operand image of one K-tile
-constexpr int P_BUF = 2 * P_OP;    // 64 KB
-constexpr int P_LDS = 2 * P_BUF;   // 128 KB of K-tile buffers
-constexpr int P_EPI = 64 * 68 * 4; // per-wave epilogue region (64 padded f32 rows)
-constexpr int P_LDS_ALLOC = P_LDS > 8 * P_EPI ? P_LDS : 8 * P_EPI;  // 136 KB
+constexpr int P_OP = PB * PK * 2;     // 32 KB: one operand image of one K-tile
+constexpr int P_BUF = 2 * P_OP;       // 64 KB
+constexpr int P_LDS = 2 * P_BUF;      // 128 KB of K-tile buffers
+constexpr int P_EROW = 72;            // epilogue staging row stride (floats): 4 rows of a pass 16 banks apart
+constexpr int P_EPI = 8 * P_EROW * 4; // per-wave epilogue staging region: 8 rows x 64 f32 (+pad)
+constexpr int P_BIAS = PB * 4;        // the tile's 256 bias values
+constexpr int P_LDS_ALLOC = P_LDS + 8 * P_EPI + P_BIAS;  // 147.5 KB
+
+// Epilogue staging reads as inline asm: the compiler cannot tell them apart from the next tile's
+// in-flight LDS-DMA targets and would put an s_waitcnt vmcnt(0) -- which also waits for every store
+// already issued -- in front of each one, serialising the store stream.  The staging region never
+// receives LDS-DMA, so only the wave's own ds_writes (in order) must precede the reads.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+// issue one 16-B staging read; lds_wait(v) (s_waitcnt lgkmcnt(0) tied to v) must precede any use of v
+__device__ __forceinline__ void lds_issue_read(const float* p, f32x4& v) {
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_addr(p)) : "memory");
+}
+__device__ __forceinline__ void lds_wait(f32x4& v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v)); }
 
 __device__ __forceinline__ void pp_barrier() {
   asm volatile("" ::: "memory");
@@ -170,33 +190,73 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wq = wave & 3;
 
+  // Persistent walk: the tiles are cut into 8 contiguous runs (one per XCD, bid & 7); the WGs of an XCD
+  // take its run's tiles round-robin, so the tiles an XCD holds at once are neighbours sharing A rows.
   const int tiles_n = p.N / PB;
   const int tiles_m = (p.M + PB - 1) / PB;
   const int nwg = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;
   const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int run0 = xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8;
+  const int run_len = q8 + (xcd < r8 ? 1 : 0);
+  const int per = (G >> 3) + (xcd < (G & 7) ? 1 : 0);  // WGs on this XCD
+  int pos = loc;
+  if (pos >= run_len) return;
+
+  const int nk = p.K / PK;
   const char* sbase = grp == 0 ? reinterpret_cast<const char*>(p.A) : reinterpret_cast<const char*>(p.W);
   uint32_t soff[8];
-  const int xcd = blockIdx.x & 7, loc = blockIdx.x >> 3;  // bijective XCD remap: each XCD a contiguous tile run
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + loc;
-  const int tm = wgid / tiles_n, tn = wgid - tm * tiles_n;
-  const int m0 = tm * PB, n0 = tn * PB;
+  int m0 = 0, n0 = 0;
   // staging sources: group 0 -> A rows m0.., group 1 -> W rows n0..; 8 x 1 KB glds per wave per K-tile
+  auto set_tile = [&](int idx, int lane) {
+    const int wg = run0 + idx;
+    const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
+    m0 = tm * PB;
+    n0 = tn * PB;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int r = 8 * (wq * 8 + i) + (lane >> 3);
-    const int c = (lane & 7) ^ ((r >> 1) & 7);
-    if (grp == 0) {
-      const int m = min(m0 + r, p.M - 1);
-      soff[i] = (uint32_t)((row_off(m, p.a_rpb, p.a_bs, p.lda) + c * 8) * 2);
-    } else {
-      soff[i] = (uint32_t)(((int64_t)(n0 + r) * p.K + c * 8) * 2);
+    for (int i = 0; i < 8; ++i) {
+      const int r = 8 * (wq * 8 + i) + (lane >> 3);
+      const int c = (lane & 7) ^ ((r >> 1) & 7);
+      if (grp == 0) {
+        const int m = min(m0 + r, p.M - 1);
+        soff[i] = (uint32_t)((row_off(m, p.a_rpb, p.a_bs, p.lda) + c * 8) * 2);
+      } else {
+        soff[i] = (uint32_t)(((int64_t)(n0 + r) * p.K + c * 8) * 2);
+      }
     }
-  }
+  };
   auto stage = [&](int t, int buf) {
     char* dst = smem + buf * P_BUF + grp * P_OP + wq * 8 * 1024;
     const char* src = sbase + (int64_t)t * (PK * 2);
 #pragma unroll
     for (int i = 0; i < 8; ++i) glds16(src + soff[i], dst + i * 1024);
+  };
+  float* bias_lds = reinterpret_cast<float*>(smem + P_LDS + 8 * P_EPI);
+  // prologue loads of a tile: A (group 0) / W (group 1) of K-tile 0, W of K-tile 1, the bias row (wave 0)
+  auto prologue = [&]() {
+    stage(0, 0);
+    if (grp == 1 && nk > 1) stage(1, 1);
+    if (wave == 0 && p.bias) glds16(p.bias + n0 + 4 * (tid & 63), reinterpret_cast<char*>(bias_lds));
+  };
+  // wait for what the first K-tile needs: every load but group 1's 8 pieces of K-tile 1 (issued after
+  // K-tile 0), and -- when ``after`` stores were issued since -- those stores too (vmcnt is in order)
+  auto prologue_wait = [&](bool stores_after) {
+    const bool w1 = grp == 1 && nk > 1;
+    if (stores_after) {
+      if constexpr (EPI != KW_EPI_RESID && sizeof(TC) == 2) {
+        if (w1) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");  // 16 epilogue stores + 8 W pieces
+        else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      } else if constexpr (EPI != KW_EPI_RESID) {
+        if (w1) asm volatile("s_waitcnt vmcnt(40)" ::: "memory");  // 32 f32 stores + 8
+        else asm volatile("s_waitcnt vmcnt(32)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else {
+      if (w1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   };
 
   // fragment read offsets (row = lane & 15 within a 16-row rep; the swizzle term (row >> 1) & 7 is per lane)
@@ -205,12 +265,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
   const int rd1 = (lane & 15) * 128 + (((1 * 4 + (lane >> 4)) ^ swz) << 4);
 
   f32x4 acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 a[8][2], b[4][2];
-
   auto read_frags = [&](int buf) {
     const char* As = smem + buf * P_BUF + grp * 128 * 128;
     const char* Bs = smem + buf * P_BUF + P_OP + wq * 64 * 128;
@@ -236,123 +291,195 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  const int nk = p.K / PK;
-  // prologue: tile 0 (both operands) and W of tile 1
-  stage(0, 0);
-  if (grp == 1 && nk > 1) stage(1, 1);
-  if (grp == 1 && nk > 1)
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  else
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  pp_barrier();
-  if (grp == 1) pp_barrier();  // the stagger
+  // The residual epilogue reads C and row_add reads a table: those loads would queue behind the next
+  // tile's prologue (vmcnt is in order), so such launches issue the prologue after the epilogue.
+  const bool overlap = EPI != KW_EPI_RESID && !p.row_add;
+  set_tile(pos, lane);
+  prologue();
+  prologue_wait(false);
 
-  if (grp == 0) {
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1;
-      read_frags(buf);
-      if (t + 1 < nk) stage(t + 1, buf ^ 1);  // A of tile t+1 (its buffer's last reader finished in slot 2t-1)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      pp_barrier();
-      mma();
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A of tile t+1 landed
-      pp_barrier();
-    }
-    pp_barrier();  // balances group 1's stagger barrier
-  } else {
-    // group 1 stages W of tile t+2 in its own read slot, after its reads of tile t drained: group 0 read
-    // tile t one slot earlier, so the buffer is free; the W of tile t+1 (issued one read slot earlier)
-    // must have landed before this slot's barrier: vmcnt(8) leaves only the 8 just-issued pieces.
-    for (int t = 0; t < nk; ++t) {
-      const int buf = t & 1;
-      read_frags(buf);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (t + 2 < nk) {
-        stage(t + 2, buf);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      pp_barrier();
-      mma();
-      pp_barrier();
-    }
-  }
+  int tcount = 0;
+  KW_GEMM_STAMP(0);
+  for (;;) {
+    // an opaque copy of the lane id per tile: keeps the epilogue's lane-derived addresses from being
+    // hoisted out of the tile loop (they would stay live across the main loop and spill)
+    int ln = lane;
+    asm volatile("" : "+v"(ln));
+    pp_barrier();
+    if (grp == 1) pp_barrier();  // the stagger
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    KW_GEMM_STAMP(1 + 3 * tcount);
 
-  // epilogue (LDS is free: every wave passed the last barrier, every glds retired).  bf16 output:
-  // 8 columns (16 B) per lane, 8 rows per store instruction; f32 (RESID / f32 store): 4 columns, 4 rows.
-  constexpr int VEC = (EPI != KW_EPI_RESID && sizeof(TC) == 2) ? 8 : 4;
-  constexpr int LPR = 64 / VEC;                  // lanes per 64-column row
-  constexpr int RPI = 64 / LPR;                  // rows per store instruction
-  float* ep = reinterpret_cast<float*>(smem + wave * P_EPI);
-  const int cq = lane % LPR;                     // this lane's VEC-column group within the wave's 64 columns
-  const int n = n0 + wq * 64 + VEC * cq;         // first of its VEC columns
-  float cb[VEC], cs[VEC];
-#pragma unroll
-  for (int e = 0; e < VEC; ++e) {
-    cb[e] = p.bias ? p.bias[n + e] : 0.f;
-    cs[e] = n + e < p.scale_cols ? p.scale : 1.f;
-  }
-  int64_t coff = n;
-  const int nb = p.M / p.hs_seq;
-  if constexpr (EPI == KW_EPI_HEADSPLIT) {
-    const int width = p.hs_heads * p.hs_hd;
-    const int part = n / width, rem = n - part * width;
-    const int h = rem / p.hs_hd, d = rem - h * p.hs_hd;
-    coff = ((int64_t)part * nb * p.hs_heads + h) * (int64_t)p.hs_seq * p.hs_hd + d;
-  }
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    // acc tiles i = 4*half .. 4*half+3 -> LDS rows 16*(i-4*half) + 4*(lane>>4) + r, column 16j + (lane&15)
-#pragma unroll
-    for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) ep[(16 * ii + 4 * (lane >> 4) + r) * 68 + 16 * j + (lane & 15)] = acc[4 * half + ii][j][r];
-#pragma unroll 4
-    for (int q = 0; q < 64 / RPI; ++q) {
-      const int rr = RPI * q + lane / LPR;
-      const int m = m0 + grp * 128 + 64 * half + rr;
-      float v[VEC];
-#pragma unroll
-      for (int e = 0; e < VEC; e += 4) {
-        const float4 v4 = *reinterpret_cast<const float4*>(ep + rr * 68 + VEC * cq + e);
-        v[e] = v4.x + cb[e]; v[e + 1] = v4.y + cb[e + 1]; v[e + 2] = v4.z + cb[e + 2]; v[e + 3] = v4.w + cb[e + 3];
+    if (grp == 0) {
+      for (int t = 0; t < nk; ++t) {
+        const int buf = t & 1;
+        read_frags(buf);
+        if (t + 1 < nk) stage(t + 1, buf ^ 1);  // A of tile t+1 (its buffer's last reader finished in slot 2t-1)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        pp_barrier();
+        mma();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A of tile t+1 landed
+        pp_barrier();
       }
-      if (m >= p.M) continue;
-      int64_t off;
-      if constexpr (EPI == KW_EPI_HEADSPLIT) {
-        const int bb = m / p.hs_seq, tt = m - bb * p.hs_seq;
-        off = (int64_t)bb * p.hs_heads * p.hs_seq * p.hs_hd + (int64_t)tt * p.hs_hd + coff;
-      } else {
-        const int bb = m / (int)p.c_rpb;
-        off = (int64_t)bb * p.c_bs + (int64_t)(m - bb * (int)p.c_rpb) * p.ldc + coff;
-      }
-      if constexpr (EPI == KW_EPI_RESID) {
-        float4* c = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off);
-        float4 o = *c;
-        o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
-        *c = o;
-      } else {
-        const float* ra = p.row_add ? p.row_add + (int64_t)(m % p.row_add_period) * p.N + n : nullptr;
-#pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          if (p.gelu) v[e] = sizeof(TC) == 2 ? gelu_bf16out(v[e]) : gelu_erf(v[e]);
-          v[e] *= cs[e];
-          if (ra) v[e] += ra[e];
-        }
-        if constexpr (sizeof(TC) == 4) {
-          *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
+      pp_barrier();  // balances group 1's stagger barrier
+    } else {
+      // group 1 stages W of tile t+2 in its own read slot, after its reads of tile t drained: group 0 read
+      // tile t one slot earlier, so the buffer is free; the W of tile t+1 (issued one read slot earlier)
+      // must have landed before this slot's barrier: vmcnt(8) leaves only the 8 just-issued pieces.
+      for (int t = 0; t < nk; ++t) {
+        const int buf = t & 1;
+        read_frags(buf);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (t + 2 < nk) {
+          stage(t + 2, buf);
+          asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
         } else {
-          uint4 o;
-          o.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-          o.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-          o.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-          o.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = o;
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        pp_barrier();
+        mma();
+        pp_barrier();
+      }
+    }
+    // every wave passed the last barrier: the K-tile buffers are free, every glds retired.  Pull this
+    // tile's bias out of LDS before the next prologue overwrites it.
+    KW_GEMM_STAMP(2 + 3 * tcount);
+    const int tm0 = m0, tn0 = n0;
+    const bool full = tm0 + PB <= p.M;
+    constexpr int VEC = (EPI != KW_EPI_RESID && sizeof(TC) == 2) ? 8 : 4;
+    constexpr int LPR = 64 / VEC;  // lanes per 64-column row
+    constexpr int RPI = 64 / LPR;  // rows per store instruction
+    const int cq = ln % LPR;     // this lane's VEC-column group within the wave's 64 columns
+    const int n = tn0 + wq * 64 + VEC * cq;
+    float cb[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; e += 4) {
+      const float4 b4 = p.bias ? *reinterpret_cast<const float4*>(bias_lds + wq * 64 + VEC * cq + e)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      cb[e] = b4.x; cb[e + 1] = b4.y; cb[e + 2] = b4.z; cb[e + 3] = b4.w;
+    }
+    pos += per;
+    const bool more = pos < run_len;
+    if (more && overlap) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      pp_barrier();  // every wave holds its bias before wave 0 restages the bias row
+      set_tile(pos, ln);
+      prologue();
+    }
+
+    // epilogue: each wave stages its 128x64 results 8 rows at a time (rows 4g + 2h + {0,1} of a 16-row
+    // tile, LDS row 2g + {0,1}) through a private region beside the K-tile buffers, then stores 16-B row
+    // pieces (8 bf16 / 4 f32): one (bf16) or two (f32) store instructions per pass.
+    float* ep = reinterpret_cast<float*>(smem + P_LDS + wave * P_EPI);
+    // per-column affine: v = acc * cmul + cadd (no GELU: bias and column scale folded), or
+    // v = gelu(acc + cadd) * cmul
+    float cmul[VEC], cadd[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      cmul[e] = n + e < p.scale_cols ? p.scale : 1.f;
+      cadd[e] = p.gelu ? cb[e] : cb[e] * cmul[e];
+    }
+    // Row -> element offset.  A 256-row tile meets at most one batch boundary when a batch holds >= 256
+    // rows (the encoder's 1500 / 3000): rows below ``bnd`` continue from rb0, the rest from rb1.
+    // Smaller batches (tests) take the general division per row.
+    int64_t coff = n;
+    const int rpb = EPI == KW_EPI_HEADSPLIT ? p.hs_seq : (int)p.c_rpb;
+    int64_t rstride, bstride;
+    if constexpr (EPI == KW_EPI_HEADSPLIT) {
+      const int nb = p.M / p.hs_seq;
+      const int width = p.hs_heads * p.hs_hd;
+      const int part = n / width, rem = n - part * width;
+      const int h = rem / p.hs_hd, d = rem - h * p.hs_hd;
+      coff = ((int64_t)part * nb * p.hs_heads + h) * (int64_t)p.hs_seq * p.hs_hd + d;
+      rstride = p.hs_hd;
+      bstride = (int64_t)p.hs_heads * p.hs_seq * p.hs_hd;
+    } else {
+      rstride = p.ldc;
+      bstride = p.c_bs;
+    }
+    const bool linear = rpb >= PB;
+    const int b0 = tm0 / rpb;
+    const int bnd = (b0 + 1) * rpb;
+    const int64_t rb0 = (int64_t)b0 * bstride + (int64_t)(tm0 - b0 * rpb) * rstride + coff;
+    const int64_t rb1 = (int64_t)(b0 + 1) * bstride + coff;
+    auto row_offset = [&](int m) -> int64_t {
+      if (linear) return m < bnd ? rb0 + (int64_t)(m - tm0) * rstride : rb1 + (int64_t)(m - bnd) * rstride;
+      const int bb = m / rpb;
+      return (int64_t)bb * bstride + (int64_t)(m - bb * rpb) * rstride + coff;
+    };
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int r2 = 0; r2 < 2; ++r2)
+            ep[(2 * (ln >> 4) + r2) * P_EROW + 16 * j + (ln & 15)] = acc[i][j][2 * hh + r2];
+#pragma unroll
+        for (int q = 0; q < 8 / RPI; ++q) {
+          const int lr = RPI * q + ln / LPR;  // LDS row 0..7
+          const int m = tm0 + grp * 128 + 16 * i + 4 * (lr >> 1) + 2 * hh + (lr & 1);
+          f32x4 v4[VEC / 4];
+          lds_issue_read(ep + lr * P_EROW + VEC * cq, v4[0]);
+          if constexpr (VEC == 8) lds_issue_read(ep + lr * P_EROW + VEC * cq + 4, v4[1]);
+          const int64_t off = row_offset(m);
+          lds_wait(v4[0]);
+          if constexpr (VEC == 8) lds_wait(v4[1]);
+          float v[VEC];
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) v[e] = v4[e >> 2][e & 3];
+          if (m >= p.M) continue;
+          if constexpr (EPI == KW_EPI_RESID) {
+            float4* c = reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off);
+            float4 o = *c;
+            o.x += v[0] + cb[0]; o.y += v[1] + cb[1]; o.z += v[2] + cb[2]; o.w += v[3] + cb[3];
+            *c = o;
+          } else {
+            if (p.gelu) {
+#pragma unroll
+              for (int e = 0; e < VEC; ++e)
+                v[e] = (sizeof(TC) == 2 ? gelu_bf16out(v[e] + cadd[e]) : gelu_erf(v[e] + cadd[e])) * cmul[e];
+            } else {
+#pragma unroll
+              for (int e = 0; e < VEC; ++e) v[e] = fmaf(v[e], cmul[e], cadd[e]);
+            }
+            if (p.row_add) {
+              const float* ra = p.row_add + (int64_t)(m % p.row_add_period) * p.N + n;
+#pragma unroll
+              for (int e = 0; e < VEC; e += 4) {
+                const float4 r4 = *reinterpret_cast<const float4*>(ra + e);
+                v[e] += r4.x; v[e + 1] += r4.y; v[e + 2] += r4.z; v[e + 3] += r4.w;
+              }
+            }
+            if constexpr (sizeof(TC) == 4) {
+              *reinterpret_cast<float4*>(reinterpret_cast<float*>(p.C) + off) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+              uint4 o;
+              o.x = pack_bf16x2(v[0], v[1]);
+              o.y = pack_bf16x2(v[2], v[3]);
+              o.z = pack_bf16x2(v[4], v[5]);
+              o.w = pack_bf16x2(v[6], v[7]);
+              *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = o;
+            }
+          }
         }
       }
+    }
+    KW_GEMM_STAMP(3 + 3 * tcount);
+    ++tcount;
+    if (!more) break;
+    if (overlap) {
+      prologue_wait(full);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      pp_barrier();  // every wave read its bias
+      set_tile(pos, ln);
+      prologue();
+      prologue_wait(false);
     }
   }
 }
@@ -425,8 +552,16 @@ hipError_t launch256_one(const GemmP& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
   const int nwg = ((p.M + PB - 1) / PB) * (p.N / PB);
-  hipLaunchKernelGGL((gemm256_kernel<EPI, TC>), dim3(nwg), dim3(512), P_LDS_ALLOC, s, p);
+  const int grid = nwg < ncu ? nwg : ncu;  // persistent: one 147.5-KB-LDS workgroup per CU
+  hipLaunchKernelGGL((gemm256_kernel<EPI, TC>), dim3(grid), dim3(512), P_LDS_ALLOC, s, p);
   return hipGetLastError();
 }
 
@@ -449,7 +584,8 @@ bool use256(const kw_gemm_args* a) {
   // vector epilogue: ldc, batch strides, head_dim in whole 16-B pieces, the C base 16-B aligned
   const int vec = (a->c_dtype == KW_DT_F32) ? 4 : 8;  // 16-B pieces: 4 f32 / 8 bf16 columns
   const bool aligned = a->ldc % vec == 0 && a->c_batch_stride % vec == 0 &&
-                       (a->hs_head_dim <= 0 || a->hs_head_dim % vec == 0) && ((uintptr_t)a->C % 16) == 0;
+                       (a->hs_head_dim <= 0 || a->hs_head_dim % vec == 0) && ((uintptr_t)a->C % 16) == 0 &&
+                       ((uintptr_t)a->row_add % 16) == 0;
   return !forced && aligned && a->N % PB == 0 && a->M >= 4 * PB;
 }
 

@@ -23,6 +23,13 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&b);
 }
 
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  // two RNE conversions in one v_cvt_pk_bf16_f32; lo in bits 0-15
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+  const bf16x2_t v = {(__bf16)lo, (__bf16)hi};
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 template <typename T> struct TypeIO;
 template <> struct TypeIO<float> {
   static __device__ __forceinline__ float ld(const float* p) { return *p; }
@@ -41,11 +48,12 @@ __device__ __forceinline__ float gelu_erf(float x) {
 __device__ __forceinline__ float gelu_bf16out(float x) {
   // GELU for a bf16 result: erf by Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7, far below bf16's
   // 2^-9 rounding) -- one rcp + one exp instead of the erff library call; f32 results use gelu_erf
-  const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  // 0.5 x (1 + sign(x) e) = h + |h| e with h = x / 2; erf(|x|/sqrt2) = e = 1 - poly(t) exp(-x^2/2)
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752440f, fabsf(x), 1.0f));
   const float poly = t * (0.254829592f + t * (-0.284496736f + t * (1.421413741f + t * (-1.453152027f + t * 1.061405429f))));
-  const float e = 1.0f - poly * __expf(-z * z);
-  return 0.5f * x * (1.0f + copysignf(e, x));
+  const float e = fmaf(-poly, __builtin_amdgcn_exp2f(x * x * -0.72134752044448170368f), 1.0f);  // -log2(e)/2
+  const float h = 0.5f * x;
+  return fmaf(fabsf(h), e, h);
 }
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -113,8 +113,34 @@ def test_gemm256_pipeline_and_epilogues(M, K):
     torch.testing.assert_close(Cb.float(), ref, atol=2e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("M,K,bias", [(33000, 64, True), (33000, 192, False), (70001, 128, True)])
+def test_gemm256_persistent(M, K, bias):
+    """More tiles than CUs: each persistent workgroup walks several tiles, the next tile's prologue
+    overlapping this one's epilogue (STORE bf16/f32); RESID and row_add take the serial hand-off."""
+    N = 1024
+    A = torch.randn(M, K, device="cuda").bfloat16()
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    b = torch.randn(N, device="cuda") if bias else None
+    ref = _ref_gemm(A, W, b)
+    Cb = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.GemmPlan(A, W, Cb, M, N, K, bias=b, gelu=True, scale=0.5, scale_cols=200)()
+    r = torch.nn.functional.gelu(ref)
+    r[:, :200] *= 0.5
+    torch.testing.assert_close(Cb.float(), r, atol=2e-2, rtol=1e-2)
+    C = torch.empty(M, N, device="cuda")
+    ops.GemmPlan(A, W, C, M, N, K, bias=b)()
+    torch.testing.assert_close(C, ref, atol=1e-3, rtol=1e-3)
+    ra = torch.randn(7, N, device="cuda")
+    ops.GemmPlan(A, W, C, M, N, K, bias=b, row_add=ra, row_add_period=7)()
+    torch.testing.assert_close(C, ref + ra[torch.arange(M, device="cuda") % 7], atol=1e-3, rtol=1e-3)
+    H0 = torch.randn(M, N, device="cuda")
+    Hc = H0.clone()
+    ops.GemmPlan(A, W, Hc, M, N, K, bias=b, epilogue=L.KW_EPI_RESID)()
+    torch.testing.assert_close(Hc, H0 + ref, atol=1e-3, rtol=1e-3)
+
+
 def test_gemm256_headsplit():
-    B, T, H, hd = 3, 1500, 4, 64
+    B, T, H, hd = 24, 1500, 4, 64  # 141 x 3 tiles: persistent walk with the head-split store
     d = H * hd
     M, N, K = B * T, 3 * d, 256
     A = torch.randn(M, K, device="cuda").bfloat16()
