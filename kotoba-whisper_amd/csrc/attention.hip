@@ -34,6 +34,17 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_base) {
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
 }
 
+// lane ^ 32 reductions by v_permlane32_swap (a VALU half-exchange; no LDS round trip like ds_bpermute):
+// with both operands = v, one result holds the lane's own value and the other its partner's
+__device__ __forceinline__ float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // ------------------------------------------------------------------------------------------------
 // encoder flash attention, bf16
 // ------------------------------------------------------------------------------------------------
@@ -116,22 +127,27 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
     }
     // mask keys >= T (last tile only), row max
     const int key0 = kt * AK;
+    if (key0 + AK > T) {  // ragged last tile only
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = key0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          if (key >= T) st[i][r] = -INFINITY;
+        }
+    }
     float mx = -INFINITY;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int key = key0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-        if (key >= T) st[i][r] = -INFINITY;
-        mx = fmaxf(mx, st[i][r]);
-      }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[i][r]);
+    mx = xor32_max(mx);
     // deferred rescale: the exponent reference m_run only moves when a score exceeds it by more than
     // 8 (p <= e^8, exact in f32 and in bf16's range); most tiles skip the O / l rescale entirely
     const bool bump = mx > m_run + 8.0f;
     if (__builtin_amdgcn_ballot_w64(bump)) {
       const float m_new = bump ? mx : m_run;
-      const float alpha = bump ? exp2f((m_run - m_new) * LOG2E) : 1.0f;
+      const float alpha = bump ? __builtin_amdgcn_exp2f((m_run - m_new) * LOG2E) : 1.0f;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -148,12 +164,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const float p = exp2f(fmaf(st[i][8 * s + e], LOG2E, mneg));
+          // raw v_exp_f32: arguments are <= 8 * log2(e) and very negative ones may flush to 0
+          const float p = __builtin_amdgcn_exp2f(fmaf(st[i][8 * s + e], LOG2E, mneg));
           rs += p;
           pf[i][s][e] = (__bf16)p;
         }
-    rs += __shfl_xor(rs, 32, 64);
-    l_run += rs;
+    l_run += xor32_sum(rs);
 
     // O^T += V^T P^T ; A operand via ds_read_b64_tr_b16 from the row-major V tile
     const int li = lane & 15, qq = li >> 2, pp = li & 3, grp = (lane >> 4) & 1;
