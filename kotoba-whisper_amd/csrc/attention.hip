@@ -24,6 +24,12 @@
 #include "kw_common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int v2u32;
+typedef __attribute__((ext_vector_type(4))) unsigned int v4u32;
+
+__device__ __forceinline__ uint32_t lds_u32(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
 
 namespace {
 
@@ -171,31 +177,42 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
         }
     l_run += xor32_sum(rs);
 
-    // O^T += V^T P^T ; A operand via ds_read_b64_tr_b16 from the row-major V tile
+    // O^T += V^T P^T ; A operand via ds_read_b64_tr_b16 from the row-major V tile.  The transposed
+    // reads are inline asm: as builtins the compiler cannot tell the V image from the next tile's
+    // in-flight LDS-DMA and puts an s_waitcnt vmcnt(0) (wait for the prefetch) in front of them.
+    // Step n = (key block i, 16-key step s) reads 4 pieces; step n+1's reads are issued before step
+    // n's MFMAs (counted lgkmcnt).
     const int li = lane & 15, qq = li >> 2, pp = li & 3, grp = (lane >> 4) & 1;
+    auto vread = [&](int n, v2u32 (&t)[2][2]) {
+      const int i = n >> 1, s = n & 1;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)        // key block
+      for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {    // 16-key step
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {  // hd block
-          bf16x8 vf;
-#pragma unroll
-          for (int half = 0; half < 2; ++half) {
-            const int row = i * 32 + 16 * s + 8 * half + 4 * hh + qq;
-            const int chunk = db * 4 + 2 * grp + (pp >> 1);
-            const int off = row * 128 + ((chunk ^ (((row >> 1) & 1) << 2)) << 4) + (pp & 1) * 8;
-            const s16x4 t = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-                (__attribute__((address_space(3))) s16x4*)(vb + off));
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              short sv = t[e];
-              vf[4 * half + e] = *reinterpret_cast<__bf16*>(&sv);
-            }
-          }
-          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[i][s], o[db], 0, 0, 0);
+        for (int half = 0; half < 2; ++half) {
+          const int row = i * 32 + 16 * s + 8 * half + 4 * hh + qq;
+          const int chunk = db * 4 + 2 * grp + (pp >> 1);
+          const int off = row * 128 + ((chunk ^ (((row >> 1) & 1) << 2)) << 4) + (pp & 1) * 8;
+          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(t[db][half]) : "v"(lds_u32(vb + off)));
         }
+    };
+    v2u32 vt[2][2][2];
+    vread(0, vt[0]);
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      if (n + 1 < 4) {
+        vread(n + 1, vt[(n + 1) & 1]);
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(vt[n & 1][0][0]), "+v"(vt[n & 1][0][1]), "+v"(vt[n & 1][1][0]),
+                     "+v"(vt[n & 1][1][1]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vt[n & 1][0][0]), "+v"(vt[n & 1][0][1]), "+v"(vt[n & 1][1][0]),
+                     "+v"(vt[n & 1][1][1]));
       }
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const v4u32 w = {vt[n & 1][db][0][0], vt[n & 1][db][0][1], vt[n & 1][db][1][0], vt[n & 1][db][1][1]};
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), pf[n >> 1][n & 1], o[db], 0, 0, 0);
+      }
+    }
   }
 
   // normalise and stage O (q rows x 64 hd, bf16) through LDS for coalesced stores
