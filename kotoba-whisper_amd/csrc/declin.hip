@@ -26,7 +26,19 @@
 
 #include "kw_common.h"
 
+// development hooks (tools/lab/declin_lab.hip records s_memrealtime stamps through them); no-ops here
+#ifndef KW_DEC_STAMP
+#define KW_DEC_STAMP_DECL
+#define KW_DEC_STAMP(slot)
+#define KW_DEC_STAMP_FLUSH
+#endif
+
 namespace {
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 0);
+}
 
 constexpr int CNT_MAX = 4096;  // seam arrival counters at the start of the workspace
 constexpr int MAXW = 8;        // waves per workgroup
@@ -58,6 +70,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
   __shared__ f32x4 red[MAXW][NCB][2][64];
   __shared__ float rpart[MAXW][32][2];  // LayerNorm: per-wave row (sum, sum of squares)
   __shared__ float rstat[32][2];     // LayerNorm: (mean, rstd) per row
+  extern __shared__ __attribute__((aligned(16))) char xs[];  // activation image (x_lds_bytes)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int cg = blockIdx.x, ks = blockIdx.y;
   const int nkt = p.K >> 5;
@@ -65,21 +78,38 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
   const int kt0 = (nkt * sl) / nsl, kt1 = (nkt * (sl + 1)) / nsl;  // <= KTM k-tiles (host-checked)
   const int ktl = max(kt1 - 1, kt0);
   const int M = p.M;
-  const int arow = lane & 15, akoff = 8 * (lane >> 4);
-  const int r0 = min(arow, M - 1), r1 = min(16 + arow, M - 1);
+  const int arow = lane & 15;
+  KW_DEC_STAMP_DECL
+  KW_DEC_STAMP(0);
 
-  // 1. every load of this wave in flight: weights (non-temporal) and activations
+  // 1. every load of this wave in flight: weights (non-temporal) into registers, and the workgroup's
+  //    activation rows x[0:32][its k-range] into LDS by LDS-DMA in whole contiguous 1-KB pieces
+  //    (the MFMA fragment pattern -- 16 rows x 64 B per load, every workgroup reading the same rows --
+  //    is 2-3x slower to land from L2 than contiguous pieces).  LDS image: 32 rows of cpr 16-B chunks
+  //    plus one pad chunk per row (odd row stride: the fragment reads are bank-conflict free).
   bf16x8 w[NCB][KTM], a0[KTM], a1[KTM];
 #pragma unroll
   for (int c = 0; c < NCB; ++c)
 #pragma unroll
     for (int u = 0; u < KTM; ++u)
       w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)(cg * NCB + c) * nkt + min(kt0 + u, ktl)) * 64 + lane);
-#pragma unroll
-  for (int u = 0; u < KTM; ++u) {
-    const int k = min(kt0 + u, ktl) * 32 + akoff;
-    a0[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r0 * p.ldx + k);
-    a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
+  const int wkt0 = (nkt * ks) / ksn, wkt1 = (nkt * (ks + 1)) / ksn;  // this workgroup's k-tiles
+  const int cpr = (wkt1 - wkt0) * 4, cprp = cpr + 1;
+  const bool xlds = ksn == 1;  // split-K workgroups read short row pieces: fragments straight from memory
+  if (xlds) {
+    const int ninst = (32 * cprp + 63) / 64;
+    const float inv = 1.0f / (float)cprp;
+    const bf16_t* xk = p.x + (int64_t)wkt0 * 32;
+    for (int j = wave; j < ninst; j += nw) {
+      const int pidx = j * 64 + lane;
+      int row = (int)(((float)pidx + 0.5f) * inv);
+      int cs = pidx - row * cprp;
+      if (cs < 0) { --row; cs += cprp; }
+      if (cs >= cprp) { ++row; cs -= cprp; }
+      if (row > 31) { row = 31; cs = 0; }  // tail of the last piece: any valid source
+      if (cs >= cpr) cs = cpr - 1;         // the pad chunk
+      glds16(xk + (int64_t)min(row, M - 1) * p.ldx + cs * 8, xs + j * 1024);
+    }
   }
   // epilogue operands of wave 0 (lane <-> column lane&15, rows 4*(lane>>4)+r and 16+...)
   float hold[NCB][2][4];
@@ -99,7 +129,27 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
     }
   }
 
+  if (xlds) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < KTM; ++u) {
+      const int pos = (arow * cprp) + (min(kt0 + u, ktl) - wkt0) * 4 + (lane >> 4);
+      a0[u] = *reinterpret_cast<const bf16x8*>(xs + pos * 16);
+      a1[u] = *reinterpret_cast<const bf16x8*>(xs + (pos + 16 * cprp) * 16);
+    }
+  } else {
+    const int r0 = min(arow, M - 1), r1 = min(16 + arow, M - 1), akoff = 8 * (lane >> 4);
+#pragma unroll
+    for (int u = 0; u < KTM; ++u) {
+      const int k = min(kt0 + u, ktl) * 32 + akoff;
+      a0[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r0 * p.ldx + k);
+      a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
+    }
+  }
+
   // 2. MFMA over this wave's k-tiles (raw operand: the LayerNorm is applied in the epilogue)
+  KW_DEC_STAMP(1);
   f32x4 c0[NCB], c1[NCB];
 #pragma unroll
   for (int c = 0; c < NCB; ++c) {
@@ -150,6 +200,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
   }
 
   // 4. reduce the waves' K slices (fixed order); wave 0 continues
+  KW_DEC_STAMP(2);
   if (nw > 1) {
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
@@ -225,6 +276,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
       }
   }
 
+  KW_DEC_STAMP(3);
   // 6. epilogue: MFMA C layout -> element (row 4*(lane>>4)+r [+16], column lane&15)
 #pragma unroll
   for (int c = 0; c < NCB; ++c) {
@@ -256,6 +308,8 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
       }
     }
   }
+  KW_DEC_STAMP(4);
+  KW_DEC_STAMP_FLUSH
 }
 
 __global__ void pack_kernel(const bf16_t* __restrict__ W, int N, int K, bf16_t* __restrict__ out) {
@@ -273,6 +327,11 @@ __global__ void pack_kernel(const bf16_t* __restrict__ W, int N, int K, bf16_t* 
     reinterpret_cast<uint4*>(out)[i] = v;
   }
 }
+
+// Dynamic LDS of the activation image for a workgroup of ``tiles`` k-tiles (32 rows x (4 tiles + 1)
+// 16-B chunks, rounded up to whole 1-KB LDS-DMA pieces).
+size_t x_lds_bytes(int tiles) { return (size_t)((32 * (4 * tiles + 1) + 63) / 64) * 1024; }
+size_t x_lds_bytes_for(int nkt, int ks) { return ks == 1 ? x_lds_bytes(nkt) : 0; }
 
 // Launch geometry for (N, K): column blocks per workgroup, k-tiles per wave, waves, K splits.
 struct Geo {
@@ -297,26 +356,29 @@ Geo choose(int64_t N, int64_t K) {
   return g;
 }
 
-template <int KTM, int NCB, bool LNA>
-hipError_t launch_store(const DecP& p, const Geo& g, bool c_f32, hipStream_t s) {
+template <int KTM, int NCB, bool LNA, int EPI, typename TC>
+hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
+  const int nkt = p.K / 32;
+  const size_t shm = x_lds_bytes_for(nkt, g.ks);
+  static size_t attr = 0;  // dynamic LDS this instantiation is cleared for
+  if (shm > attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dec_linear_kernel<KTM, NCB, LNA, EPI, TC>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+    attr = shm;
+  }
   const dim3 grid((unsigned)((p.N + 16 * NCB - 1) / (16 * NCB)), (unsigned)g.ks);
   const dim3 block((unsigned)(64 * g.nw));
-  if (c_f32)
-    hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, KW_EPI_STORE, float>), grid, block, 0, s, p, g.ks);
-  else
-    hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, KW_EPI_STORE, bf16_t>), grid, block, 0, s, p, g.ks);
+  hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, EPI, TC>), grid, block, shm, s, p, g.ks);
   return hipGetLastError();
 }
 
 template <int KTM, int NCB>
 hipError_t launch_k(const DecP& p, bool resid, const Geo& g, bool c_f32, hipStream_t s) {
-  const dim3 grid((unsigned)((p.N + 16 * NCB - 1) / (16 * NCB)), (unsigned)g.ks);
-  const dim3 block((unsigned)(64 * g.nw));
-  if (resid) {  // (no LayerNorm-fused residual linear in the decoder)
-    hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, false, KW_EPI_RESID, float>), grid, block, 0, s, p, g.ks);
-    return hipGetLastError();
-  }
-  return p.ln ? launch_store<KTM, NCB, true>(p, g, c_f32, s) : launch_store<KTM, NCB, false>(p, g, c_f32, s);
+  if (resid) return launch_one<KTM, NCB, false, KW_EPI_RESID, float>(p, g, s);  // (no LayerNorm-fused residual linear)
+  if (p.ln)
+    return c_f32 ? launch_one<KTM, NCB, true, KW_EPI_STORE, float>(p, g, s) : launch_one<KTM, NCB, true, KW_EPI_STORE, bf16_t>(p, g, s);
+  return c_f32 ? launch_one<KTM, NCB, false, KW_EPI_STORE, float>(p, g, s) : launch_one<KTM, NCB, false, KW_EPI_STORE, bf16_t>(p, g, s);
 }
 
 hipError_t launch(const DecP& p, bool resid, const Geo& g, bool c_f32, hipStream_t s) {
@@ -333,8 +395,9 @@ extern "C" size_t kw_dec_linear_workspace_bytes(int64_t N, int64_t K) {
 }
 
 extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
-  if (!a || !a->x || !a->W || a->M < 0 || a->N <= 0 || a->K <= 0 || a->K % 32 != 0 || a->ldx % 8 != 0 || a->ldx < a->K)
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: null pointer or bad sizes (K % 32 == 0, ldx % 8 == 0)");
+  if (!a || !a->x || !a->W || a->M < 0 || a->N <= 0 || a->K <= 0 || a->K % 32 != 0 || a->ldx % 8 != 0 || a->ldx < a->K ||
+      (uintptr_t)a->x % 16 != 0)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: null pointer or bad sizes (K % 32 == 0, ldx % 8 == 0, x 16-B aligned)");
   if (a->epilogue == KW_EPI_RESID) {
     if (!a->h || !a->hb || a->ldh < a->N)
       return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: RESID needs h (f32) and hb (bf16) with ldh >= N");
