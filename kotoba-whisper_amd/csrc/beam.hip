@@ -45,9 +45,11 @@ __global__ __launch_bounds__(ST) void beam_logprobs_kernel(kw_beam_logprobs_args
 
   // log_softmax normaliser of the raw row: lp = (x - max) - log(sum exp(x - max))
   float m = -INFINITY;
+#pragma unroll 8
   for (int v = tid; v < V; v += ST) m = fmaxf(m, x[v]);
   m = block_reduce_max(m, shf);
   float s = 0.f;
+#pragma unroll 8
   for (int v = tid; v < V; v += ST) s += expf(x[v] - m);
   s = block_reduce_sum(s, shf);
   const float ls = logf(s);

@@ -63,6 +63,7 @@ struct DecP {
   int M, N, K;
   float* slab;
   int* cnt;
+  int xlds;  // stage the activation rows through LDS (single-round, no-split-K grids)
 };
 
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
@@ -95,7 +96,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
       w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)(cg * NCB + c) * nkt + min(kt0 + u, ktl)) * 64 + lane);
   const int wkt0 = (nkt * ks) / ksn, wkt1 = (nkt * (ks + 1)) / ksn;  // this workgroup's k-tiles
   const int cpr = (wkt1 - wkt0) * 4, cprp = cpr + 1;
-  const bool xlds = ksn == 1;  // split-K workgroups read short row pieces: fragments straight from memory
+  const bool xlds = p.xlds;
   if (xlds) {
     const int ninst = (32 * cprp + 63) / 64;
     const float inv = 1.0f / (float)cprp;
@@ -331,7 +332,7 @@ __global__ void pack_kernel(const bf16_t* __restrict__ W, int N, int K, bf16_t* 
 // Dynamic LDS of the activation image for a workgroup of ``tiles`` k-tiles (32 rows x (4 tiles + 1)
 // 16-B chunks, rounded up to whole 1-KB LDS-DMA pieces).
 size_t x_lds_bytes(int tiles) { return (size_t)((32 * (4 * tiles + 1) + 63) / 64) * 1024; }
-size_t x_lds_bytes_for(int nkt, int ks) { return ks == 1 ? x_lds_bytes(nkt) : 0; }
+
 
 // Launch geometry for (N, K): column blocks per workgroup, k-tiles per wave, waves, K splits.
 struct Geo {
@@ -356,10 +357,16 @@ Geo choose(int64_t N, int64_t K) {
   return g;
 }
 
+// LDS staging pays where one round of workgroups covers the grid (its 80-114 KB of LDS allows one
+// workgroup per CU) and K is not split (split-K workgroups read short row pieces); the LM head's
+// 1,621-workgroup grid keeps direct fragment loads at four workgroups per CU.
+bool use_xlds(int64_t N, const Geo& g) { return g.ks == 1 && (N + 16 * g.ncb - 1) / (16 * g.ncb) <= 256; }
+size_t x_lds_bytes_for(int nkt, bool xlds) { return xlds ? x_lds_bytes(nkt) : 0; }
+
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
 hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
   const int nkt = p.K / 32;
-  const size_t shm = x_lds_bytes_for(nkt, g.ks);
+  const size_t shm = x_lds_bytes_for(nkt, p.xlds);
   static size_t attr = 0;  // dynamic LDS this instantiation is cleared for
   if (shm > attr) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dec_linear_kernel<KTM, NCB, LNA, EPI, TC>),
@@ -444,6 +451,7 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     p.ldh = a->ldh;
     p.cnt = reinterpret_cast<int*>(a->workspace);
     p.slab = a->workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(a->workspace) + CNT_MAX * sizeof(int)) : nullptr;
+    p.xlds = use_xlds(a->N, g) ? 1 : 0;
     hipError_t e = launch(p, a->epilogue == KW_EPI_RESID, g, a->c_dtype == KW_DT_F32, s);
     if (e != hipSuccess) return kw_set_error(e);
   }

@@ -121,6 +121,7 @@ __device__ __forceinline__ void timestamp_rule(RowState& st, const uint8_t* mask
                                                int V, F f, float* shf) {
   const int tid = threadIdx.x;
   float m_all = -INFINITY, m_text = -INFINITY, m_ts = -INFINITY;
+#pragma unroll 8
   for (int v = tid; v < V; v += ST) {
     const float s = process(st, mask, bsup, nbsup, v, f(v));
     m_all = fmaxf(m_all, s);
@@ -130,6 +131,7 @@ __device__ __forceinline__ void timestamp_rule(RowState& st, const uint8_t* mask
   m_text = block_reduce_max(m_text, shf);
   m_ts = block_reduce_max(m_ts, shf);
   float sum = 0.f;
+#pragma unroll 8
   for (int v = tid; v < V; v += ST) {
     const float s = process(st, mask, bsup, nbsup, v, f(v));
     sum += expf(s - m_all);

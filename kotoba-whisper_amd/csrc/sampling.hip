@@ -36,12 +36,27 @@ __global__ __launch_bounds__(ST) void greedy_step_kernel(kw_sampler_args a) {
   if (st.rt) timestamp_rule(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, V, [&](int v) { return x[v]; }, shf);
 
   // ---- argmax (first index on ties) -----------------------------------------------------------
+  // 8 loads of the logits and the suppress mask in flight per thread before any compare (a one-load
+  // loop pays an L2 round trip per 4 KB of the row)
   float best = -INFINITY;
   int bi = 0x7fffffff;
-  for (int v = tid; v < V; v += ST) {
-    const float s = process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, x[v]);
-    if (a.scores_out) a.scores_out[(int64_t)b * a.V + v] = s;
-    if (s > best || (s == best && v < bi)) { best = s; bi = v; }
+  constexpr int UNR = 8;
+  for (int v0 = tid; v0 < V; v0 += ST * UNR) {
+    float xv[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int v = v0 + u * ST;
+      xv[u] = v < V ? x[v] : -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int v = v0 + u * ST;
+      if (v < V) {
+        const float s = process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, xv[u]);
+        if (a.scores_out) a.scores_out[(int64_t)b * a.V + v] = s;
+        if (s > best || (s == best && v < bi)) { best = s; bi = v; }
+      }
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {

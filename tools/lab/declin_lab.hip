@@ -29,7 +29,8 @@ float run(const char* name, DecP p, int nw, int ks, std::vector<const bf16x8*>& 
   dim3 grid((p.N + 16 * NCB - 1) / (16 * NCB), ks), block(64 * nw);
   hipGraph_t g; hipGraphExec_t ge;
   CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
-  const size_t shm = x_lds_bytes_for(p.K / 32, ks);
+  p.xlds = ks == 1 && (int)grid.x <= 256;
+  const size_t shm = x_lds_bytes_for(p.K / 32, p.xlds);
   CK(hipFuncSetAttribute(reinterpret_cast<const void*>(&dec_linear_kernel<KTM, NCB, LNA, EPI, TC>),
                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   for (auto* W : Ws) { p.W = W; hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, EPI, TC>), grid, block, shm, s, p, ks); }
