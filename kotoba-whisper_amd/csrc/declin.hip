@@ -112,8 +112,16 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
       glds16(xk + (int64_t)min(row, M - 1) * p.ldx + cs * 8, xs + j * 1024);
     }
   }
-  // epilogue operands of wave 0 (lane <-> column lane&15, rows 4*(lane>>4)+r and 16+...)
-  float hold[NCB][2][4];
+  // epilogue operands of wave 0 (lane <-> column lane&15, rows 4*(lane>>4)+r and 16+...), loaded with
+  // the operands so the epilogue never waits on a memory round trip: bias, LayerNorm column sums and
+  // (RESID) the residual rows
+  float hold[NCB][2][4], ebias[NCB], ecsum[NCB];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
+    ebias[c] = p.bias ? p.bias[n] : 0.f;
+    ecsum[c] = LNA ? p.ln_colsum[n] : 0.f;
+  }
   if constexpr (EPI == KW_EPI_RESID) {
     if (wave == 0) {
 #pragma unroll
@@ -284,8 +292,8 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
     const int cb = cg * NCB + c;
     const int n = cb * 16 + (lane & 15);
     const bool nvalid = n < p.N;
-    const float bn = (p.bias && nvalid) ? p.bias[n] : 0.f;
-    const float cs = (LNA && nvalid) ? p.ln_colsum[n] : 0.f;
+    const float bn = ebias[c];
+    const float cs = ecsum[c];
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
 #pragma unroll
