@@ -54,12 +54,19 @@ class DecodeSession:
                                    dtype=torch.float32)
         self._graph = None
         self._graph_key = None
+        self._cross_key = None
         if enc is not None:
             self.set_encoder_output(enc)
 
     # ------------------------------------------------------------------------------------------
-    def set_encoder_output(self, enc: torch.Tensor) -> None:
+    def set_encoder_output(self, enc: torch.Tensor, key=None) -> None:
+        """Project ``enc`` into every layer's cross K/V.  ``key`` (optional) names the encoder output: a
+        repeat call with the key of the K/V already held skips the projection (the v3 multi-task loop
+        decodes several prompts against one encoder pass, run_pseudo_labelling_v3.py:309-321)."""
+        if key is not None and key == self._cross_key:
+            return
         self.eng.cross_kv(enc, self.B, out=self.cross)
+        self._cross_key = key
 
     def _buffers(self, q: int):
         if q not in self._bufs:

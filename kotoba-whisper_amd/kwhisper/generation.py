@@ -79,6 +79,8 @@ class KWhisperForConditionalGeneration:
         self.generation_config = engine.generation_config
         self._sessions = {}
         self.stats = {}
+        self._memo = None  # generate_multitask's per-batch encoder memo
+        self._memo_count = 0
 
     # ---- nn.Module-ish surface used by callers ---------------------------------------------------
     @property
@@ -235,18 +237,29 @@ class KWhisperForConditionalGeneration:
             time_offset = seek.astype(np.float64) * 0.02 / 2
             seek_num = np.minimum(max_frames - seek, nseg)
             if feats is not None:
-                if shortform and total == nseg and all(seek[p] == 0 for p in batch_map) and cur == B:
+                whole = shortform and total == nseg and all(seek[p] == 0 for p in batch_map) and cur == B
+                if whole:
                     seg_in = feats
                 else:
                     seg_in = torch.zeros((cur, feats.shape[1], nseg), device=eng.device, dtype=torch.float32)
                     for i, p in enumerate(batch_map):
                         n = int(seek_num[p])
                         seg_in[i, :, :n] = feats[p, :, int(seek[p]): int(seek[p]) + n]
-                enc = eng.encode(seg_in)
+                enc_key = None
+                memo = self._memo
+                if memo is not None and whole and passes == 0:
+                    # multi-task reuse: the first pass of every prompt sees the same mel, so the encoder and
+                    # the cross-K/V projection run once per batch (clone: later passes reuse the buffer)
+                    if "enc" not in memo:
+                        memo["enc"] = eng.encode(seg_in).clone()
+                    enc, enc_key = memo["enc"], ("memo", memo["id"])
+                else:
+                    enc = eng.encode(seg_in)
             else:
                 if passes > 0:
                     raise NotImplementedError("encoder_outputs with a multi-pass seek loop")
                 enc = eh.to(eng.device, eng.dtype).reshape(B * s.max_source_positions, s.d_model).contiguous()
+                enc_key = None
             prompt = prompt_all[batch_map]
             if max_new_tokens is None:
                 max_length = min(max_length + min(s.max_target_positions // 2 - 1, P), s.max_target_positions)
@@ -254,7 +267,7 @@ class KWhisperForConditionalGeneration:
             else:
                 eff_max = P + max_new_tokens
             sess = self._session(cur, num_beams)
-            sess.set_encoder_output(enc)
+            sess.set_encoder_output(enc, key=enc_key)
             if num_beams > 1:
                 ids = sess.generate_beam(torch.from_numpy(prompt), gen, num_beams=num_beams, max_length=eff_max,
                                          return_timestamps=return_timestamps, length_penalty=length_penalty,
@@ -290,6 +303,24 @@ class KWhisperForConditionalGeneration:
         if return_segments or (return_dict_in_generate and return_timestamps):
             return {"sequences": res, "segments": segments}
         return res
+
+    def generate_multitask(self, input_features, tasks, **kwargs):
+        """``generate`` once per (language, task) of ``tasks`` on the same features -- the inner loop of
+        run_pseudo_labelling_v3.py:309-318 -- with ONE encoder pass and ONE cross-K/V projection shared by
+        every prompt.  Each result is exactly what ``generate(input_features,
+        language=..., task=..., **kwargs)`` returns on its own; only passes after the first (the
+        timestamp seek loop's re-encodes of shifted mel) run the encoder again."""
+        if not tasks:
+            return []
+        for k in ("language", "task", "encoder_outputs"):
+            if k in kwargs:
+                raise ValueError(f"generate_multitask takes `{k}` from `tasks`, not as a keyword")
+        self._memo_count += 1
+        self._memo = {"id": self._memo_count}
+        try:
+            return [self.generate(input_features, language=lang, task=task, **kwargs) for lang, task in tasks]
+        finally:
+            self._memo = None
 
     # ---- helpers ------------------------------------------------------------------------------------
     def detect_language(self, input_features=None, encoder_outputs=None, generation_config=None):

@@ -19,7 +19,8 @@ from typing import Callable, Iterable, List, Optional, Sequence
 import numpy as np
 import torch
 
-__all__ = ["shard_batches", "gather_remainder", "pad_across_processes", "pseudo_label", "write_transcription_csv"]
+__all__ = ["shard_batches", "gather_remainder", "pad_across_processes", "pseudo_label", "pseudo_label_multitask",
+           "legacy_prompt", "write_transcription_csv", "transcription_table", "write_transcription_arrow"]
 
 
 def shard_batches(n_items: int, batch_size: int, world: int, rank: int) -> List[List[int]]:
@@ -101,37 +102,103 @@ def _all_gather_rows(t: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts, 0)
 
 
+def legacy_prompt(generation_config, language: str, task: str = "transcribe", return_timestamps: bool = False):
+    """The init tokens older transformers (4.35, the reference's pin ``requirements.txt:2``) left at the start
+    of every generated row: ``[sot, lang, task]`` plus ``notimestamps`` without timestamps
+    (generation_whisper.py:1591-1603).  The legacy consumer ``run_data_filtering.py:230-251,279`` reads the
+    task tokens at ``timestamp_position = 3`` of each row."""
+    from .config import language_to_id
+
+    g = generation_config
+    row = [g.decoder_start_token_id, language_to_id(language, g), g.task_to_id[task]]
+    if not return_timestamps:
+        row.append(g.no_timestamps_token_id)
+    return row
+
+
+def _with_prompt(ids: torch.Tensor, prompt: Sequence[int]) -> torch.Tensor:
+    pre = torch.tensor(list(prompt), dtype=ids.dtype, device=ids.device).expand(ids.shape[0], len(prompt))
+    return torch.cat([pre, ids], 1)
+
+
+def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode):
+    """Shared DP loop: ``decode(feats)`` -> list of id matrices (one per output column); each is padded
+    across ranks and gathered with the file ids (``run_pseudo_labelling.py:336-344``, v3 ``:309-321``)."""
+    dist = _dist()
+    world = dist.get_world_size() if dist else 1
+    rank = dist.get_rank() if dist else 0
+    steps = shard_batches(n_items, batch_size, world, rank)
+    rem = gather_remainder(n_items, batch_size, world)
+    eval_ids: List[int] = []
+    cols: Optional[List[List[np.ndarray]]] = None
+    for si, idx in enumerate(steps):
+        outs = decode(features(idx))
+        if cols is None:
+            cols = [[] for _ in outs]
+        last = si == len(steps) - 1 and rem > 0
+        fid = None
+        for c, ids in enumerate(outs):
+            ids = ids.to(comm_device) if comm_device is not None else ids
+            ids = _all_gather_rows(pad_across_processes(ids, pad_token_id))
+            if fid is None:
+                fid = _all_gather_rows(torch.tensor(idx, dtype=torch.int64, device=ids.device))
+                if last:
+                    fid = fid[:rem]
+                eval_ids.extend(int(x) for x in fid.cpu().tolist())
+            if last:
+                ids = ids[:rem]
+            cols[c].extend(ids.cpu().numpy())
+        if on_step is not None:
+            on_step(si, len(steps))
+    return eval_ids, cols or []
+
+
 def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *, batch_size: int,
                  gen_kwargs: Optional[dict] = None, pad_token_id: int = 50256, comm_device=None,
-                 on_step: Optional[Callable[[int, int], None]] = None):
+                 on_step: Optional[Callable[[int, int], None]] = None, legacy_prompt_in_output: bool = False):
     """Transcribe items 0..n_items-1 data-parallel; returns (item_indices, predictions) in dataset order
     on every rank (``run_pseudo_labelling.py:333-344``).
 
     ``features(indices)`` returns the (b, n_mels, 3000) log-mel batch for those dataset indices (on the
     model's device); ``predictions`` is a list of 1-D int64 numpy arrays, one per item, each padded to
-    its gather round's common width exactly as the reference's ``eval_preds`` rows are."""
-    dist = _dist()
-    world = dist.get_world_size() if dist else 1
-    rank = dist.get_rank() if dist else 0
+    its gather round's common width exactly as the reference's ``eval_preds`` rows are.
+    ``legacy_prompt_in_output`` prepends ``legacy_prompt(...)`` to every row (needs ``language``)."""
     gen_kwargs = dict(gen_kwargs or {})
-    steps = shard_batches(n_items, batch_size, world, rank)
-    rem = gather_remainder(n_items, batch_size, world)
-    eval_ids: List[int] = []
-    eval_preds: List[np.ndarray] = []
-    for si, idx in enumerate(steps):
-        feats = features(idx)
+    prompt = None
+    if legacy_prompt_in_output:
+        if not gen_kwargs.get("language"):
+            raise ValueError("legacy_prompt_in_output needs an explicit `language` in gen_kwargs")
+        prompt = legacy_prompt(model.generation_config, gen_kwargs["language"], gen_kwargs.get("task") or "transcribe",
+                               bool(gen_kwargs.get("return_timestamps")))
+
+    def decode(feats):
         ids = model.generate(feats, **gen_kwargs)
-        ids = ids.to(comm_device) if comm_device is not None else ids
-        ids = pad_across_processes(ids, pad_token_id)
-        fid = torch.tensor(idx, dtype=torch.int64, device=ids.device)
-        ids, fid = _all_gather_rows(ids), _all_gather_rows(fid)
-        if si == len(steps) - 1 and rem > 0:
-            ids, fid = ids[:rem], fid[:rem]
-        eval_preds.extend(ids.cpu().numpy())
-        eval_ids.extend(int(x) for x in fid.cpu().tolist())
-        if on_step is not None:
-            on_step(si, len(steps))
-    return eval_ids, eval_preds
+        return [_with_prompt(ids, prompt) if prompt else ids]
+
+    eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode)
+    return eval_ids, (cols[0] if cols else [])
+
+
+def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *,
+                           batch_size: int, text_lang_task: Sequence[tuple], gen_kwargs: Optional[dict] = None,
+                           pad_token_id: int = 50256, comm_device=None,
+                           on_step: Optional[Callable[[int, int], None]] = None):
+    """``run_pseudo_labelling_v3.py:299-321``: every batch is decoded once per (text, lang, task) triple.
+    Returns (item_indices, {text: predictions}) in dataset order; ``whisper_<text>`` is the column the
+    reference adds (:322-323).  The encoder and cross-K/V run once per batch (``generate_multitask``) when
+    the model offers it, so each extra task costs only its decode loop."""
+    gen_kwargs = dict(gen_kwargs or {})
+    tasks = [(lang, task) for _, lang, task in text_lang_task]
+
+    def decode(feats):
+        if hasattr(model, "generate_multitask"):
+            return model.generate_multitask(feats, tasks, **gen_kwargs)
+        return [model.generate(feats, language=lang, task=task, **gen_kwargs) for lang, task in tasks]
+
+    eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode)
+    if not cols:
+        cols = [[] for _ in text_lang_task]
+    return eval_ids, {t[0]: c for t, c in zip(text_lang_task, cols)}
 
 
 def write_transcription_csv(path: str, file_ids: Iterable[str], preds: Iterable[np.ndarray]) -> None:
@@ -141,3 +208,24 @@ def write_transcription_csv(path: str, file_ids: Iterable[str], preds: Iterable[
         w = csv.writer(f)
         w.writerow(["file_id", "whisper_transcript"])
         w.writerows([[fid, p] for fid, p in zip(file_ids, preds)])
+
+
+def transcription_table(file_ids: Iterable[str], preds: Iterable[np.ndarray], column: str = "whisper_transcript"):
+    """The pseudo-label Arrow column the reference appends to the dataset
+    (``raw_datasets["train"].add_column("whisper_transcript", eval_preds)``, run_pseudo_labelling.py:351):
+    ``list<int64>`` token rows, keyed by ``file_id``."""
+    import pyarrow as pa
+
+    rows = [np.asarray(p, dtype=np.int64) for p in preds]
+    return pa.table({"file_id": pa.array(list(file_ids), type=pa.string()),
+                     column: pa.array([r.tolist() for r in rows], type=pa.list_(pa.int64()))})
+
+
+def write_transcription_arrow(path: str, file_ids: Iterable[str], preds: Iterable[np.ndarray],
+                              column: str = "whisper_transcript") -> None:
+    """Write ``transcription_table`` as an Arrow IPC stream file (the format of ``datasets``' cache files)."""
+    import pyarrow as pa
+
+    table = transcription_table(file_ids, preds, column)
+    with pa.OSFile(path, "wb") as sink, pa.ipc.new_stream(sink, table.schema) as w:
+        w.write_table(table)

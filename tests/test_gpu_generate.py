@@ -160,3 +160,77 @@ def test_large_bf16_vs_reference(gold):
     assert err.mean() < 0.1
     del model, sess
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("ts", [False, True])
+def test_generate_multitask_reuses_encoder(gold, tiny32, ts):
+    """SURVEY §8f row 4 (run_pseudo_labelling_v3.py:309-321): generate_multitask == one generate() per
+    (language, task), bit-exact, with the first-pass encoder run once for all prompts (later seek-loop
+    passes re-encode shifted mel per prompt, as the reference does)."""
+    g = gold("tiny_fp32")
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    tasks = [("ja", "transcribe"), ("ja", "translate"), ("en", "transcribe")]
+    eng = tiny32.engine
+    calls = []
+    orig = eng.encode
+
+    def counting(mel):
+        calls.append(mel.shape[0])
+        return orig(mel)
+
+    eng.encode = counting
+    try:
+        want = [tiny32.generate(feats, language=l, task=t, return_timestamps=ts).cpu() for l, t in tasks]
+        n_separate = len(calls)
+        calls.clear()
+        got = tiny32.generate_multitask(feats, tasks, return_timestamps=ts)
+        n_multi = len(calls)
+        again = tiny32.generate(feats, language="ja", task="transcribe", return_timestamps=ts).cpu()
+    finally:
+        del eng.encode
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.numpy())
+    np.testing.assert_array_equal(again.numpy(), want[0].numpy())  # the memo does not leak into plain calls
+    assert n_multi == n_separate - (len(tasks) - 1), (n_multi, n_separate)
+
+
+@pytest.mark.parametrize("ts", [False, True])
+def test_asr_pipeline_chunked(tiny32, ts):
+    """ASRPipeline (chunk_length_s=15, batch_size=3, two clips of 40 s and 7 s) equals the
+    reference composition chunk by chunk: transformers' chunk_iter windows -> generate() one window at a
+    time -> transformers' own _decode_asr merge (stub tokenizer, see test_pipeline.py)."""
+    from transformers.models.whisper.tokenization_whisper import _decode_asr
+    from transformers.pipelines.automatic_speech_recognition import chunk_iter as hf_chunk_iter
+
+    from kwhisper.feature_extraction import WhisperFeatureExtractor
+    from kwhisper.pipeline import ASRPipeline
+    from kwhisper.synthetic import dummy_audio
+    from test_pipeline import StubTokenizer
+
+    tk = StubTokenizer()
+    tk.all_special_ids = tk.all_special_ids + [tiny32.generation_config.pad_token_id]
+    long = np.concatenate([dummy_audio(i) for i in range(2)])[: 16000 * 40].astype(np.float32)
+    clips = [long, long[: 16000 * 7]]
+    gk = dict(language="ja", task="transcribe", max_length=40)
+    pipe = ASRPipeline(tiny32, tokenizer=tk, chunk_length_s=15, batch_size=3, generate_kwargs=gk)
+    got = pipe([{"array": c, "sampling_rate": 16000, "path": f"c{i}"} for i, c in enumerate(clips)],
+               return_timestamps=ts)
+    fe = WhisperFeatureExtractor(feature_size=TINY.num_mel_bins)
+
+    class _FE:
+        sampling_rate = 16000
+
+        def __call__(self, chunk, **kw):
+            return {"chunk": chunk}
+
+    for clip, res in zip(clips, got):
+        outputs = []
+        for item in hf_chunk_iter(clip, _FE(), 240000, 40000, 40000):
+            feats = fe(item["chunk"])["input_features"]
+            ids = tiny32.generate(feats, return_timestamps=ts, **gk).cpu()
+            n, left, right = item["stride"]
+            outputs.append({"tokens": ids, "stride": (n / 16000, left / 16000, right / 16000)})
+        text, optional = _decode_asr(tk, outputs, return_timestamps=ts, return_language=None, time_precision=0.02)
+        assert res["text"] == text and len(text) > 0
+        assert res.get("chunks") == optional.get("chunks")
+        assert "path" not in res  # a datasets audio dict's path is dropped (automatic_speech_recognition.py:391-393)

@@ -1,0 +1,159 @@
+"""ASR pipeline path (kwhisper.pipeline) against transformers' own functions, CPU only.
+
+* ``chunk_iter`` == TF/pipelines/automatic_speech_recognition.py ``chunk_iter`` (windows, strides, is_last);
+* ``find_longest_common_sequence`` == tokenization_whisper ``_find_longest_common_sequence`` on
+  overlapping random windows;
+* ``decode_asr`` == tokenization_whisper ``_decode_asr`` driven by a stub tokenizer (no vocab files
+  offline: the stub decodes ids to "[id]" strings and knows the Whisper special ids), over synthetic
+  chunk outputs with timestamps, strides, language tokens and prompts.
+The GPU end-to-end test lives in test_gpu_generate.py.
+"""
+import numpy as np
+import pytest
+
+from kwhisper.config import LANGUAGES, TINY, generation_constants
+from kwhisper.pipeline import chunk_iter, decode_asr, find_longest_common_sequence
+
+asr = pytest.importorskip("transformers.pipelines.automatic_speech_recognition")
+tw = pytest.importorskip("transformers.models.whisper.tokenization_whisper")
+
+G = generation_constants(TINY)
+TS = G.no_timestamps_token_id + 1
+
+
+class StubTokenizer:
+    """What _decode_asr asks of a Whisper tokenizer, for the multilingual v1/v2 vocabulary."""
+
+    def __init__(self, g=G):
+        self.g = g
+        self.all_special_ids = list(range(g.eos_token_id, g.no_timestamps_token_id + 1))
+        self._names = {g.eos_token_id: "endoftext", g.decoder_start_token_id: "startoftranscript",
+                       g.prev_sot_token_id: "startofprev", g.no_timestamps_token_id: "notimestamps",
+                       g.task_to_id["translate"]: "translate", g.task_to_id["transcribe"]: "transcribe"}
+        for tok, tid in g.lang_to_id.items():
+            self._names[tid] = tok[2:-2]
+
+    def convert_tokens_to_ids(self, tok):
+        inv = {f"<|{v}|>": k for k, v in self._names.items()}
+        return inv[tok]
+
+    def decode(self, ids):
+        ids = [int(i) for i in ids]
+        if len(ids) == 1 and ids[0] in self._names:
+            return f"<|{self._names[ids[0]]}|>"
+        return "".join(f"[{i}]" for i in ids)
+
+    def _strip_prompt(self, token_ids, prompt_token_id, decoder_start_token_id):
+        return tw.WhisperTokenizer._strip_prompt(self, token_ids, prompt_token_id, decoder_start_token_id)
+
+    @staticmethod
+    def _convert_to_list(token_ids):
+        return tw.WhisperTokenizer._convert_to_list(token_ids)
+
+
+def _vocab(tk):
+    lang_of = {tid: dict(LANGUAGES)[tok[2:-2]] for tok, tid in G.lang_to_id.items()}
+    return dict(timestamp_begin=TS, special_ids=tk.all_special_ids, lang_of=lang_of,
+                prompt_token_id=G.prev_sot_token_id, decoder_start_token_id=G.decoder_start_token_id,
+                decode=tk.decode)
+
+
+class _FE:
+    sampling_rate = 16000
+
+    def __call__(self, chunk, **kw):
+        return {"n": chunk.shape[0]}
+
+
+@pytest.mark.parametrize("n", [0, 1, 1000, 16000 * 5, 16000 * 15, 16000 * 15 + 1, 16000 * 31, 16000 * 62 + 7])
+@pytest.mark.parametrize("cl,sl,sr", [(240000, 40000, 40000), (480000, 80000, 80000), (16000, 4000, 2000),
+                                      (100, 0, 0), (100, 50, 50)])
+def test_chunk_iter_matches_transformers(n, cl, sl, sr):
+    audio = np.zeros(n, dtype=np.float32)
+    if cl - sl - sr <= 0:
+        return  # the reference raises ("Chunk length must be superior to stride length") before iterating
+    want = [(d["is_last"], d["stride"], d["n"]) for d in asr.chunk_iter(audio, _FE(), cl, sl, sr)]
+    got = [(last, st, b - a) for a, b, last, st in chunk_iter(n, cl, sl, sr)]
+    assert got == want
+
+
+def _windows(rng, n_total, n_win, overlap, noise):
+    seq = rng.integers(0, 500, n_total).tolist()
+    step = max(1, n_total // n_win)
+    out = []
+    for s in range(0, n_total, step):
+        w = seq[max(0, s - overlap): s + step + overlap]
+        w = [t if rng.random() > noise else int(rng.integers(0, 500)) for t in w]
+        out.append(w)
+    return out
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_longest_common_sequence_matches_transformers(seed):
+    rng = np.random.default_rng(seed)
+    wins = _windows(rng, int(rng.integers(1, 120)), int(rng.integers(1, 6)), int(rng.integers(0, 12)),
+                    float(rng.choice([0.0, 0.1, 0.4])))
+    if seed % 7 == 0:
+        wins.append([])
+    assert find_longest_common_sequence(wins) == tw._find_longest_common_sequence(wins)
+
+
+def _chunk_tokens(rng, with_ts, prompt, lang_tok, L=30):
+    toks = []
+    if prompt:
+        toks += [G.prev_sot_token_id, 11, 12, G.decoder_start_token_id]
+    if lang_tok:
+        toks += [lang_tok, G.task_to_id["transcribe"]]
+    t = 0
+    while len(toks) < L:
+        if with_ts:
+            t += int(rng.integers(0, 60))
+            toks.append(TS + min(t, 1500))
+            toks += rng.integers(0, 400, int(rng.integers(1, 6))).tolist()
+            t += int(rng.integers(0, 80))
+            toks.append(TS + min(t, 1500))
+            if rng.random() < 0.2 and toks[-1] > TS:
+                toks.append(toks[-1])  # duplicate-timestamp quirk
+        else:
+            toks += rng.integers(0, 400, 4).tolist()
+    if rng.random() < 0.3:
+        toks.append(G.eos_token_id)
+    return np.asarray([toks], dtype=np.int64)
+
+
+@pytest.mark.parametrize("seed", range(60))
+def test_decode_asr_matches_transformers(seed):
+    rng = np.random.default_rng(seed)
+    tk = StubTokenizer()
+    with_ts = bool(seed % 2)
+    n_chunks = int(rng.integers(1, 5))
+    langs = [G.lang_to_id["<|ja|>"], G.lang_to_id["<|en|>"], None]
+    outputs = []
+    for c in range(n_chunks):
+        lt = langs[int(rng.integers(0, 3))] if seed % 3 == 0 else None
+        o = {"tokens": _chunk_tokens(rng, with_ts, prompt=(seed % 5 == 0 and c == 0), lang_tok=lt)}
+        if seed % 4 != 1:  # strided (chunked) or not
+            left = 0.0 if c == 0 else 2.5
+            right = 0.0 if c == n_chunks - 1 else 2.5
+            o["stride"] = (15.0, left, right)
+        outputs.append(o)
+    rl = seed % 3 == 0
+    ref_outputs = [dict(o) for o in outputs]
+    want = tw._decode_asr(tk, ref_outputs, return_timestamps=with_ts, return_language=rl, time_precision=0.02)
+    got = decode_asr([dict(o) for o in outputs], return_timestamps=with_ts, return_language=rl,
+                     time_precision=0.02, **_vocab(tk))
+    assert got == want
+
+
+def test_decode_asr_token_mode():
+    """Without a tokenizer the merge returns token ids (the text of each chunk is its id list)."""
+    tk = StubTokenizer()
+    rng = np.random.default_rng(3)
+    outputs = [{"tokens": _chunk_tokens(rng, False, False, None), "stride": (15.0, 0.0 if c == 0 else 2.5,
+                                                                             2.5 if c < 2 else 0.0)}
+               for c in range(3)]
+    v = _vocab(tk)
+    text, _ = decode_asr(outputs, return_timestamps=False, time_precision=0.02, **v)
+    v["decode"] = None
+    toks, _ = decode_asr(outputs, return_timestamps=False, time_precision=0.02, **v)
+    assert text == tk.decode(toks)

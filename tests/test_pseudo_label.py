@@ -110,3 +110,109 @@ def test_transcription_csv_format(tmp_path):
     rows = list(csv.reader(open(p, encoding="UTF8")))
     assert rows[0] == ["file_id", "whisper_transcript"]
     assert rows[1] == ["a.flac", str(preds[0])] and rows[2] == ["b.flac", str(preds[1])]
+
+
+class _StubTaskModel(_StubModel):
+    """generate() whose output depends on the (language, task) prompt: row i -> tokens offset by the task."""
+
+    OFF = {("ja", "transcribe"): 0, ("en", "translate"): 1000}
+
+    def generate(self, feats, language=None, task=None, **kw):
+        out = super().generate(feats, **kw)
+        return torch.where(out == PAD, out, out + self.OFF[(language, task)])
+
+
+TLT = [("transcription", "ja", "transcribe"), ("translation", "en", "translate")]
+
+
+def test_multitask_columns_match_separate_runs():
+    """run_pseudo_labelling_v3.py:309-321: one prediction column per (text, lang, task) triple, each equal
+    to a single-task run with that prompt."""
+    from kwhisper.pseudo_label import pseudo_label_multitask
+
+    m = _StubTaskModel()
+    ids, cols = pseudo_label_multitask(m, _features, 13, batch_size=4, text_lang_task=TLT, pad_token_id=PAD)
+    assert ids == list(range(13)) and set(cols) == {"transcription", "translation"}
+    for text, lang, task in TLT:
+        ids1, preds1 = pseudo_label(m, _features, 13, batch_size=4, pad_token_id=PAD,
+                                    gen_kwargs=dict(language=lang, task=task))
+        assert ids1 == ids
+        for a, b in zip(cols[text], preds1):
+            np.testing.assert_array_equal(a, b)
+
+
+def _mt_worker(rank, world, port, n, bs, out_dir):
+    import torch.distributed as dist
+
+    from kwhisper.pseudo_label import pseudo_label_multitask
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ids, cols = pseudo_label_multitask(_StubTaskModel(), _features, n, batch_size=bs, text_lang_task=TLT,
+                                           pad_token_id=PAD)
+        np.savez(os.path.join(out_dir, f"mt{rank}.npz"), ids=np.array(ids),
+                 **{t: np.array([p.tolist() + [-1] * (16 - len(p)) for p in c]) for t, c in cols.items()})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_multitask_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+
+    from kwhisper.pseudo_label import pseudo_label_multitask
+
+    n, bs = 11, 4
+    mp.spawn(_mt_worker, args=(2, _free_port(), n, bs, str(tmp_path)), nprocs=2, join=True)
+    _, ref = pseudo_label_multitask(_StubTaskModel(), _features, n, batch_size=bs, text_lang_task=TLT,
+                                    pad_token_id=PAD)
+    for r in range(2):
+        z = np.load(tmp_path / f"mt{r}.npz")
+        assert z["ids"].tolist() == list(range(n))
+        for text, _, _ in TLT:
+            for i in range(n):
+                row = z[text][i][z[text][i] != -1]
+                k = len(ref[text][i][ref[text][i] != PAD])
+                np.testing.assert_array_equal(row[:k], ref[text][i][:k])
+                assert (row[k:] == PAD).all()
+
+
+@pytest.mark.parametrize("ts", [False, True])
+def test_legacy_prompt_in_output(ts):
+    """rows start with [sot, lang, task] (+ notimestamps), the layout
+    run_data_filtering.py:230-251,279 indexes with timestamp_position = 3."""
+    from kwhisper.config import LARGE_V3, generation_constants
+
+    class M(_StubModel):
+        generation_config = generation_constants(LARGE_V3)
+
+    g = M.generation_config
+    _, plain = pseudo_label(M(), _features, 6, batch_size=4, pad_token_id=PAD,
+                            gen_kwargs=dict(language="ja", task="transcribe", return_timestamps=ts))
+    _, leg = pseudo_label(M(), _features, 6, batch_size=4, pad_token_id=PAD, legacy_prompt_in_output=True,
+                          gen_kwargs=dict(language="ja", task="transcribe", return_timestamps=ts))
+    pre = [50258, 50266, 50360] + ([] if ts else [50364])
+    assert [g.decoder_start_token_id, g.lang_to_id["<|ja|>"], g.task_to_id["transcribe"]] == pre[:3]
+    for a, b in zip(plain, leg):
+        assert b[: len(pre)].tolist() == pre
+        np.testing.assert_array_equal(b[len(pre):], a)
+    with pytest.raises(ValueError):
+        pseudo_label(M(), _features, 2, batch_size=4, legacy_prompt_in_output=True, gen_kwargs={})
+
+
+def test_transcription_arrow_column_matches_datasets(tmp_path):
+    """The Arrow column equals what datasets' add_column("whisper_transcript", eval_preds) stores
+    (run_pseudo_labelling.py:351), and the IPC file reads back to the same table."""
+    pa = pytest.importorskip("pyarrow")
+    datasets = pytest.importorskip("datasets")
+    from kwhisper.pseudo_label import transcription_table, write_transcription_arrow
+
+    preds = [np.array([50258, 50266, 50360, 123, PAD]), np.array([7, 8, 9, PAD, PAD])]
+    fids = ["a.flac", "b.flac"]
+    ds = datasets.Dataset.from_dict({"file_id": fids}).add_column("whisper_transcript", preds)
+    t = transcription_table(fids, preds)
+    assert t.column("whisper_transcript").to_pylist() == ds["whisper_transcript"][:]
+    p = str(tmp_path / "labels.arrow")
+    write_transcription_arrow(p, fids, preds)
+    with pa.OSFile(p, "rb") as f:
+        back = pa.ipc.open_stream(f).read_all()
+    assert back.equals(t)

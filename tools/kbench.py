@@ -61,6 +61,7 @@ def main():
     ap.add_argument("--layers", type=int, default=32)
     ap.add_argument("--only", default="", help="comma list of kernel names to run (default: all)")
     ap.add_argument("--eager", action="store_true", help="no graph, no timing (for rocprofv3 --pmc passes)")
+    ap.add_argument("--warm", action="store_true", help="one weight buffer per linear (L2/MALL-warm replays)")
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
@@ -79,7 +80,7 @@ def main():
                                    ("lm_head", 51866, d, True, False)]:
         if not want(name):
             continue
-        n_bufs = 1 if name == "lm_head" else nl
+        n_bufs = 1 if (name == "lm_head" or a.warm) else nl
         Ws = [ops.pack_weight((torch.randn(N, K, device=dev) / K ** 0.5).bfloat16()) for _ in range(n_bufs)]
         cs = torch.zeros(N, device=dev)
         bias = torch.zeros(N, device=dev)
