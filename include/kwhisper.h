@@ -126,6 +126,11 @@ size_t kw_packed_weight_bytes(int64_t N, int64_t K);
  * of :398,407 fused in front of the next LayerNorm). */
 int kw_layernorm(float* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
                  float eps, void* y, int y_dtype, const void* delta, kw_stream_t stream);
+/* The same over a bf16 residual stream x [rows][dim] (the encoder's bf16 path): x += delta is rounded
+ * to bf16, as the reference's residual add in a bf16 model is. dim % 8 == 0, dim <= 2048, x/y/delta
+ * 16-B aligned. */
+int kw_layernorm_bf16res(void* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
+                         float eps, void* y, int y_dtype, const void* delta, kw_stream_t stream);
 
 /* Encoder self-attention softmax(Q K^T) V (q pre-scaled; TF sdpa_attention.py:79-166, non-causal).
  * qkv: [3][B][H][T][hd] (dtype), out: [B][T][H*hd] (dtype). hd == 64. */

@@ -73,6 +73,98 @@ __global__ __launch_bounds__(256) void layernorm_kernel(float* __restrict__ x, i
   }
 }
 
+// ---- The same over a bf16 residual stream (the encoder's bf16 path): 16-B accesses of 8 elements, the
+// row held in registers.  x += delta is rounded to bf16 -- the reference's residual add in a bf16 model
+// (modeling_whisper.py:398,407 under torch_dtype=bfloat16) -- and the LayerNorm reads the rounded sum.
+constexpr int LNB_MAXV = 4;  // 8-element chunks per lane -> dim <= 64*8*4 = 2048
+
+template <typename TOut>
+__global__ __launch_bounds__(256) void layernorm_bf16res_kernel(bf16_t* __restrict__ x, int64_t rows, int dim,
+                                                                const float* __restrict__ g,
+                                                                const float* __restrict__ bta, float eps,
+                                                                TOut* __restrict__ y, const bf16_t* __restrict__ delta) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  uint4* xr = reinterpret_cast<uint4*>(x + row * dim);
+  const uint4* dr = delta ? reinterpret_cast<const uint4*>(delta + row * dim) : nullptr;
+  const int nv = dim >> 3;
+  uint4 raw[LNB_MAXV], draw[LNB_MAXV];
+#pragma unroll
+  for (int i = 0; i < LNB_MAXV; ++i) {  // every load of the row in flight first
+    const int c = i * 64 + lane;
+    if (c < nv) {
+      raw[i] = xr[c];
+      if (dr) draw[i] = dr[c];
+    }
+  }
+  float v[LNB_MAXV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LNB_MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nv) {
+      const uint32_t w[4] = {raw[i].x, raw[i].y, raw[i].z, raw[i].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        v[i][2 * e] = __uint_as_float(w[e] << 16);
+        v[i][2 * e + 1] = __uint_as_float(w[e] & 0xffff0000u);
+      }
+      if (dr) {
+        const uint32_t d[4] = {draw[i].x, draw[i].y, draw[i].z, draw[i].w};
+        uint32_t o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[i][2 * e] = bf2f(f2bf(v[i][2 * e] + __uint_as_float(d[e] << 16)));
+          v[i][2 * e + 1] = bf2f(f2bf(v[i][2 * e + 1] + __uint_as_float(d[e] & 0xffff0000u)));
+          o[e] = pack_bf16x2(v[i][2 * e], v[i][2 * e + 1]);
+        }
+        xr[c] = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s += v[i][e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[i][e] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)dim;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LNB_MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nv) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float a = v[i][e] - mean;
+        q = fmaf(a, a, q);
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)dim + eps);
+  TOut* yr = y + row * dim;
+#pragma unroll
+  for (int i = 0; i < LNB_MAXV; ++i) {
+    const int c = i * 64 + lane;
+    if (c < nv) {
+      const float4 g0 = reinterpret_cast<const float4*>(g)[2 * c], g1 = reinterpret_cast<const float4*>(g)[2 * c + 1];
+      const float4 b0 = reinterpret_cast<const float4*>(bta)[2 * c], b1 = reinterpret_cast<const float4*>(bta)[2 * c + 1];
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = (v[i][e] - mean) * rstd * gg[e] + bb[e];
+      if constexpr (sizeof(TOut) == 4) {
+        reinterpret_cast<float4*>(yr)[2 * c] = make_float4(o[0], o[1], o[2], o[3]);
+        reinterpret_cast<float4*>(yr)[2 * c + 1] = make_float4(o[4], o[5], o[6], o[7]);
+      } else {
+        reinterpret_cast<uint4*>(yr)[c] = make_uint4(pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3]),
+                                                     pack_bf16x2(o[4], o[5]), pack_bf16x2(o[6], o[7]));
+      }
+    }
+  }
+}
+
 // ---- mel [B][C][T] f32 -> [B][T+2][c_pad] (zero time padding rows and zero channel padding) ----
 template <typename TOut>
 __global__ __launch_bounds__(256) void mel_tm_kernel(const float* __restrict__ mel, int C, int T, int c_pad,
@@ -127,6 +219,24 @@ extern "C" int kw_layernorm(float* x, int64_t rows, int64_t dim, const float* ga
   else
     hipLaunchKernelGGL(layernorm_kernel<bf16_t>, grid, dim3(256), 0, s, x, rows, (int)dim, gamma, beta, eps, (bf16_t*)y,
                        (const bf16_t*)delta);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}
+
+extern "C" int kw_layernorm_bf16res(void* x, int64_t rows, int64_t dim, const float* gamma, const float* beta,
+                                    float eps, void* y, int y_dtype, const void* delta, kw_stream_t stream) {
+  if (!x || !gamma || !beta || !y || rows < 0 || dim <= 0 || dim % 8 != 0 || dim > 64 * 8 * LNB_MAXV ||
+      (uintptr_t)x % 16 != 0 || (uintptr_t)y % 16 != 0 || (delta && (uintptr_t)delta % 16 != 0))
+    return kw_set_error_msg(KW_EINVAL, "kw_layernorm_bf16res: invalid arguments (dim % 8 == 0, dim <= 2048, 16-B aligned)");
+  if (rows == 0) return KW_OK;
+  hipStream_t s = (hipStream_t)stream;
+  dim3 grid((unsigned)((rows + 3) / 4));
+  if (y_dtype == KW_DT_F32)
+    hipLaunchKernelGGL(layernorm_bf16res_kernel<float>, grid, dim3(256), 0, s, (bf16_t*)x, rows, (int)dim, gamma, beta,
+                       eps, (float*)y, (const bf16_t*)delta);
+  else
+    hipLaunchKernelGGL(layernorm_bf16res_kernel<bf16_t>, grid, dim3(256), 0, s, (bf16_t*)x, rows, (int)dim, gamma, beta,
+                       eps, (bf16_t*)y, (const bf16_t*)delta);
   KW_CHECK_LAUNCH();
   return KW_OK;
 }

@@ -13,7 +13,7 @@ import os
 
 import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkwhisper.so")
+LIB_PATH = os.environ.get("KWHISPER_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkwhisper.so")
 
 KW_OK, KW_EINVAL, KW_EHIP, KW_EUNSUPPORTED = 0, 1, 2, 3
 KW_DT_F32, KW_DT_BF16 = 0, 1
@@ -95,6 +95,8 @@ EXPORTS = {
     "kw_pack_weight": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "kw_packed_weight_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
     "kw_layernorm": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp, c_vp]),
+    "kw_layernorm_bf16res": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp,
+                                            c_vp]),
     "kw_attention": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp]),
     "kw_embed": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_vp, c_vp, c_vp, c_i64, c_vp, c_vp, c_vp]),
     "kw_self_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,

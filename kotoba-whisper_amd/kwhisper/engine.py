@@ -5,7 +5,9 @@ encoder :592-646, decoder :690-795, proj_out :1080.  Every op is a kwhisper HIP 
 C ABI; torch only owns memory, streams and graph capture.
 
 Layout in HBM (DESIGN.md §Data layout):
-  * residual stream f32 [rows][d]; GEMM inputs (LayerNorm outputs) in the compute dtype;
+  * encoder residual stream [rows][d]: bf16 on the bf16 path (the reference's bf16 model keeps it in
+    bf16; the LayerNorm adds the producing linear's bf16 output into it), f32 in the parity mode;
+    decoder residual f32 with a bf16 mirror; GEMM inputs (LayerNorm outputs) in the compute dtype;
   * conv stem: mel -> time-major zero-padded [B][3002][c_pad], conv1 output [B][3002][d]
     (pad rows stay zero), so both convolutions are im2col-free GEMMs;
   * encoder q/k/v head-split [3][B][H][1500][64]; cross-attention K/V of all decoder layers from ONE
@@ -38,7 +40,9 @@ class _EncoderBuffers:
         self.B = B
         self.mel_tm = torch.empty((B, s.n_frames + 2, eng.c_pad), device=dev, dtype=dt)
         self.conv = torch.zeros((B, s.n_frames + 2, d), device=dev, dtype=dt)  # pad rows stay zero
-        self.h = torch.empty((B * T, d), device=dev, dtype=torch.float32)
+        # residual stream: f32 in the parity mode; bf16 on the bf16 path -- the reference model's own
+        # residual precision (run_pseudo_labelling.py:229 loads the teacher in bfloat16)
+        self.h = torch.empty((B * T, d), device=dev, dtype=torch.float32 if dt == torch.float32 else dt)
         self.x = torch.empty((B * T, d), device=dev, dtype=dt)
         self.qkv = torch.empty((3 * B * T * d,), device=dev, dtype=dt)
         self.attn = torch.empty((B * T, d), device=dev, dtype=dt)
@@ -53,7 +57,7 @@ class _EncoderBuffers:
 class WhisperEngine:
     """The MI355X Whisper model: ``encode`` (mel -> hidden) and decode sessions.
 
-    ``dtype`` = torch.bfloat16 (performance path, bf16 MFMA, f32 accumulation and residual) or
+    ``dtype`` = torch.bfloat16 (performance path, bf16 MFMA with f32 accumulation) or
     torch.float32 (parity path: exact-fp32 MFMA; greedy tokens match the fp32 reference).
     """
 

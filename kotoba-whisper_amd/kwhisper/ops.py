@@ -73,16 +73,21 @@ def mel_to_time_major(mel: torch.Tensor, c_pad: int, dtype: torch.dtype, out: to
 
 def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, out: torch.Tensor,
               delta: torch.Tensor | None = None):
-    """out = LayerNorm(x) (x f32); with ``delta`` (bf16, x's shape) x += delta first, in place."""
+    """out = LayerNorm(x); with ``delta`` (bf16, x's shape) x += delta first, in place.  x is the residual
+    stream: f32 (kw_layernorm) or bf16 (kw_layernorm_bf16res, the sum rounded to bf16)."""
     _cuda(x, gamma, beta, out, delta)
-    if x.dtype != torch.float32 or not x.is_contiguous():
-        raise ValueError("layernorm input must be contiguous float32")
+    if x.dtype not in (torch.float32, torch.bfloat16) or not x.is_contiguous():
+        raise ValueError("layernorm input must be contiguous float32 or bfloat16")
     if delta is not None and (delta.dtype != torch.bfloat16 or delta.numel() != x.numel() or not delta.is_contiguous()):
         raise ValueError("layernorm delta must be a contiguous bf16 tensor of x's size")
     dim = x.shape[-1]
     rows = x.numel() // dim
-    L.check(_lib().kw_layernorm(_p(x), rows, dim, _p(gamma), _p(beta), eps, _p(out), _dt(out), _p(delta), _s()),
-            "kw_layernorm")
+    if x.dtype == torch.bfloat16:
+        L.check(_lib().kw_layernorm_bf16res(_p(x), rows, dim, _p(gamma), _p(beta), eps, _p(out), _dt(out), _p(delta),
+                                            _s()), "kw_layernorm_bf16res")
+    else:
+        L.check(_lib().kw_layernorm(_p(x), rows, dim, _p(gamma), _p(beta), eps, _p(out), _dt(out), _p(delta), _s()),
+                "kw_layernorm")
     return out
 
 

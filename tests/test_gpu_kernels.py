@@ -246,6 +246,25 @@ def test_layernorm(rows, dim, out_dtype):
     torch.testing.assert_close(y.float(), ref, atol=tol * 4, rtol=tol)
 
 
+@pytest.mark.parametrize("rows,dim", [(3, 384), (48000, 1280), (5, 2048), (2, 8)])
+@pytest.mark.parametrize("with_delta", [False, True])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_layernorm_bf16_residual(rows, dim, with_delta, out_dtype):
+    """bf16 residual stream (encoder bf16 path): x = bf16(x + delta) written back bit-exactly, then the
+    LayerNorm of the rounded sum (torch fp32/f64 references of the same op)."""
+    x = (torch.randn(rows, dim, device="cuda") * 3 + 1).to(torch.bfloat16)
+    delta = (torch.randn(rows, dim, device="cuda") * 2).to(torch.bfloat16) if with_delta else None
+    g = torch.randn(dim, device="cuda")
+    b = torch.randn(dim, device="cuda")
+    want_h = (x.float() + delta.float()).to(torch.bfloat16) if with_delta else x.clone()
+    y = torch.empty(rows, dim, device="cuda", dtype=out_dtype)
+    ops.layernorm(x, g, b, 1e-5, y, delta=delta)
+    assert torch.equal(x, want_h)
+    ref = torch.nn.functional.layer_norm(want_h.double(), (dim,), g.double(), b.double(), 1e-5).float()
+    tol = 1e-5 if out_dtype == torch.float32 else 2e-2
+    torch.testing.assert_close(y.float(), ref, atol=tol * 4, rtol=tol)
+
+
 @pytest.mark.parametrize("rows,dim", [(3, 384), (48000, 1280)])
 def test_layernorm_residual_delta(rows, dim):
     """x += delta (bf16, written back) then LayerNorm: the encoder's fused residual add."""
