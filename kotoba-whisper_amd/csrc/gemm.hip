@@ -17,6 +17,10 @@
 #include "gemm_common.h"
 
 // development hook (tools/lab/gemm_lab.hip defines it to record s_memtime stamps); no-op here
+#ifndef KW_GEMM_GM
+#define KW_GEMM_GM 4  // row tiles per group in gemm256's tile order (1 = row-major)
+#endif
+
 #ifndef KW_GEMM_STAMP
 #define KW_GEMM_STAMP(slot)
 #endif
@@ -211,7 +215,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
   // staging sources: group 0 -> A rows m0.., group 1 -> W rows n0..; 8 x 1 KB glds per wave per K-tile
   auto set_tile = [&](int idx, int lane) {
     const int wg = run0 + idx;
-    const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
+    // grouped order: KW_GEMM_GM row tiles walk the columns together, so the ~32 tiles an XCD holds at
+    // once span GM row blocks x (32 / GM) column blocks and share both operands in its L2
+    const int per_group = KW_GEMM_GM * tiles_n;
+    const int gidx = wg / per_group;
+    const int first_m = gidx * KW_GEMM_GM;
+    const int gm = min(KW_GEMM_GM, tiles_m - first_m);
+    const int rr = wg - gidx * per_group;
+    const int tm = first_m + rr % gm, tn = rr / gm;
     m0 = tm * PB;
     n0 = tn * PB;
 #pragma unroll
