@@ -62,6 +62,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=2)
     ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--pipeline", action="store_true",
+                    help="generate_pipelined: the next batch's log-mel/encoder/cross-K/V on CUs [0, --encoder-cus) "
+                         "beside this batch's decode (measured slower on 1x MI355X: profiles/r01e_lab_notes.md)")
+    ap.add_argument("--encoder-cus", type=int, default=64)
     return ap.parse_args()
 
 
@@ -93,21 +97,29 @@ def main():
     gen_kw = dict(language="ja", task="transcribe", max_length=a.max_length, return_timestamps=False)
     out_ids = []
 
-    def step():
-        feats = fe.extract(audio)
-        ids = model.generate(feats, **gen_kw)
-        out_ids.append(ids)
-        return ids
+    if not a.pipeline:
+        def batches(n):
+            for _ in range(n):
+                yield model.generate(fe.extract(audio), **gen_kw)
+    else:
+        # one generator over warmup + timed batches: the first timed batch's encoder already ran beside the
+        # last warmup decode, as every later batch's runs beside its predecessor's (steady state)
+        stream_of = model.generate_pipelined((audio for _ in range(a.warmup + a.steps)), feature_extractor=fe,
+                                             encoder_cus=a.encoder_cus, **gen_kw)
 
-    for _ in range(a.warmup):
-        step()
+        def batches(n):
+            for _ in range(n):
+                yield next(stream_of)
+
+    for ids in batches(a.warmup):
+        out_ids.append(ids)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for ids in batches(a.steps):
+        out_ids.append(ids)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -131,7 +143,7 @@ def main():
 
     # ---- per-kernel measurements (HIP events on the launching stream, after the timed region) ----
     eng = model.engine
-    sess = model._sessions[(B, 1)]
+    sess = model._sessions.get((B, 1)) or model._sessions[(B, 1, 1)]
     stream = torch.cuda.current_stream(dev)
     iters = a.kernel_iters
 
@@ -179,6 +191,7 @@ def main():
         "config": {"workload": "config 3: whisper-large-v3 greedy generate, 30 s clips, log-mel on GPU",
                    "model": shape.name, "global_batch": B * world, "per_gpu_batch": B,
                    "max_length": a.max_length, "new_tokens": new_tokens, "seq_len": 1500,
+                   "pipelined": a.pipeline, "encoder_cus": a.encoder_cus if a.pipeline else None,
                    "parallelism": f"dp{world}"},
         "roofline": {"kernel": "cross_attn_partial (decoder cross-attention K/V stream, per layer)",
                      "bound": "hbm", "achieved": cross_bytes / cross_t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -32,6 +32,11 @@ enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 int kw_version(void);  /* 102 */
 const char* kw_last_error(void);
 
+/* A stream whose kernels run only on CUs [cu_begin, cu_end) (hipExtStreamCreateWithCUMask), and its
+ * release.  Used to run the next batch's encoder beside the current batch's decode steps. */
+int kw_stream_create_cu_range(int cu_begin, int cu_end, kw_stream_t* out);
+int kw_stream_destroy(kw_stream_t stream);
+
 /* a1 -- log-mel spectrogram.
  * Replaces WhisperFeatureExtractor._torch_extract_fbank_features (TF/models/whisper/
  * feature_extraction_whisper.py:135-168): stft(n_fft 400, hop 160, periodic hann, center, reflect)

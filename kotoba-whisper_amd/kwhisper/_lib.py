@@ -86,6 +86,8 @@ class BeamSelectArgs(ctypes.Structure):
 
 EXPORTS = {
     "kw_version": (ctypes.c_int, []),
+    "kw_stream_create_cu_range": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_vp)]),
+    "kw_stream_destroy": (ctypes.c_int, [c_vp]),
     "kw_last_error": (ctypes.c_char_p, []),
     "kw_log_mel": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp, c_vp, c_vp]),
     "kw_mel_to_time_major": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp]),

@@ -55,6 +55,8 @@ class DecodeSession:
         self._graph = None
         self._graph_key = None
         self._cross_key = None
+        self._greedy_cfg = {}
+        self._pinned = None
         if enc is not None:
             self.set_encoder_output(enc)
 
@@ -215,20 +217,33 @@ class DecodeSession:
         self.unfinished.fill_(1)
         self.counter.zero_()
         self.n_unfinished.fill_(B)
-        sup = torch.zeros((self.eng.shape.vocab_size,), dtype=torch.uint8)
-        if gen.suppress_tokens:
-            sup[torch.tensor(gen.suppress_tokens)] = 1
-        self._sup = sup.to(dev)
-        self._bsup = torch.tensor(gen.begin_suppress_tokens or [0], dtype=torch.int32, device=dev)
-        nb = len(gen.begin_suppress_tokens or [])
+        # the sampler plan, its processor tables and the captured step graph are kept per configuration:
+        # a repeat call (the next batch) replays the same graph -- no re-capture, whose device-wide
+        # synchronize would also wait for an encoder running beside this decode (generate_pipelined)
+        key = (max_length, P, bool(return_timestamps), tuple(gen.suppress_tokens or ()),
+               tuple(gen.begin_suppress_tokens or ()), gen.timestamp_begin, gen.no_timestamps_token_id,
+               gen.eos_token_id, gen.pad_token_id, gen.max_initial_timestamp_index, bool(record_scores))
+        cfg = self._greedy_cfg.get(key)
+        if cfg is None:
+            sup = torch.zeros((self.eng.shape.vocab_size,), dtype=torch.uint8)
+            if gen.suppress_tokens:
+                sup[torch.tensor(gen.suppress_tokens)] = 1
+            sup = sup.to(dev)
+            bsup = torch.tensor(gen.begin_suppress_tokens or [0], dtype=torch.int32, device=dev)
+            nb = len(gen.begin_suppress_tokens or [])
+            score_buf = torch.empty_like(self.logits) if record_scores else None
+            sampler = ops.SamplerPlan(self.logits, sup, bsup if nb else None, self.ids, self.cur_len,
+                                      self.unfinished, self.counter, self.n_unfinished,
+                                      return_timestamps=return_timestamps, ts_begin=gen.timestamp_begin,
+                                      no_ts_id=gen.no_timestamps_token_id, eos_id=gen.eos_token_id,
+                                      pad_id=gen.pad_token_id, max_initial_ts=gen.max_initial_timestamp_index,
+                                      max_length=max_length, begin_index=P, scores_out=score_buf)
+            cfg = dict(sampler=sampler, score_buf=score_buf, graph=None)
+            if len(self._greedy_cfg) >= 8:  # bound the cache (each entry may hold a graph)
+                self._greedy_cfg.pop(next(iter(self._greedy_cfg)))
+            self._greedy_cfg[key] = cfg
+        sampler, score_buf = cfg["sampler"], cfg["score_buf"]
         self.scores = [] if record_scores else None
-        score_buf = torch.empty_like(self.logits) if record_scores else None
-        sampler = ops.SamplerPlan(self.logits, self._sup, self._bsup if nb else None, self.ids, self.cur_len,
-                                  self.unfinished, self.counter, self.n_unfinished,
-                                  return_timestamps=return_timestamps, ts_begin=gen.timestamp_begin,
-                                  no_ts_id=gen.no_timestamps_token_id, eos_id=gen.eos_token_id,
-                                  pad_id=gen.pad_token_id, max_initial_ts=gen.max_initial_timestamp_index,
-                                  max_length=max_length, begin_index=P, scores_out=score_buf)
         # prefill
         self._run(self._step_plans(P))
         sampler()
@@ -242,17 +257,21 @@ class DecodeSession:
             self._run(step_seq)
             sampler()
 
-        graph = None
-        if use_graph and not record_scores and n_steps > 1:
-            key = (max_length, P, return_timestamps, id(sampler))
+        graph = cfg["graph"]
+        if graph is None and use_graph and not record_scores and n_steps > 1:
             graph = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.graph(graph, stream=side):
                 one_step()
             torch.cuda.current_stream(dev).wait_stream(side)
-            self._graph, self._graph_key = graph, key
-        pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
+            cfg["graph"] = graph
+        if not use_graph:
+            graph = None
+        self._graph, self._graph_key = graph, key
+        if self._pinned is None or self._pinned.numel() < check_every + 1:
+            self._pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
+        pinned = self._pinned
         events = []
         while done < n_steps:
             if graph is not None:

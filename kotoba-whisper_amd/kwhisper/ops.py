@@ -335,3 +335,11 @@ class BeamStepPlan:
     def __call__(self):
         L.check(_lib().kw_beam_logprobs(self._ra, _s()), "kw_beam_logprobs")
         L.check(_lib().kw_beam_select(self._rb, _s()), "kw_beam_select")
+
+
+def cu_range_stream(cu_begin: int, cu_end: int) -> torch.cuda.ExternalStream:
+    """A torch stream over a HIP stream restricted to CUs [cu_begin, cu_end) (kw_stream_create_cu_range).
+    The stream lives as long as the process (it is handed to torch as an external stream)."""
+    h = ctypes.c_void_p()
+    L.check(_lib().kw_stream_create_cu_range(int(cu_begin), int(cu_end), ctypes.byref(h)), "kw_stream_create_cu_range")
+    return torch.cuda.ExternalStream(h.value)

@@ -234,3 +234,25 @@ def test_asr_pipeline_chunked(tiny32, ts):
         assert res["text"] == text and len(text) > 0
         assert res.get("chunks") == optional.get("chunks")
         assert "path" not in res  # a datasets audio dict's path is dropped (automatic_speech_recognition.py:391-393)
+
+
+@pytest.mark.parametrize("ts", [False, True])
+def test_generate_pipelined_matches_per_batch(gold, tiny32, ts):
+    """generate_pipelined (next batch's log-mel + encoder + cross-K/V on a CU-restricted stream beside this
+    batch's decode) yields exactly generate() per batch; with timestamps it runs batch by batch."""
+    from kwhisper.feature_extraction import WhisperFeatureExtractor
+    from kwhisper.synthetic import dummy_audio
+
+    fe = WhisperFeatureExtractor(feature_size=TINY.num_mel_bins)
+    audio = [torch.from_numpy(np.stack([dummy_audio(10 * k + i) for i in range(3)])).cuda() for k in range(4)]
+    kw = dict(language="ja", task="transcribe", max_length=32, return_timestamps=ts)
+    want = [tiny32.generate(fe.extract(a), **kw).cpu() for a in audio]
+    got = list(tiny32.generate_pipelined(audio, feature_extractor=fe, encoder_cus=64, **kw))
+    assert len(got) == len(want)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.numpy())
+    feats = [fe.extract(a) for a in audio[:2]]
+    got2 = list(tiny32.generate_pipelined(feats, **kw))  # features in, no extractor
+    for a, b in zip(got2, want[:2]):
+        np.testing.assert_array_equal(a.cpu().numpy(), b.numpy())
+    assert list(tiny32.generate_pipelined([], **kw)) == []

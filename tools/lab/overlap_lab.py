@@ -81,21 +81,16 @@ def run(name, fns):
 
 
 full = torch.cuda.Stream()
+hi = torch.cuda.Stream(priority=-1)
 g_full = capture(full)
+g_hi = capture(hi)
 run("decode x%d alone (full chip)" % NSTEP, [lambda: decode(g_full, full)])
 run("encoder + cross-KV alone (full chip)", [lambda: encoder(full)])
 run("serial: encoder then decode (full chip)", [lambda: encoder(full), lambda: decode(g_full, full)])
-layouts = {
-    "low": lambda n: range(n),
-    "strided": lambda n: [i for i in range(NCU) if (i % (NCU // n if n else 1)) == 0][:n],
-}
-for n_enc in (32, 64, 96):
-    for lay, f in layouts.items():
-        eb = list(f(n_enc))
-        db = [i for i in range(NCU) if i not in set(eb)]
-        se, sdm = masked_stream(eb), masked_stream(db)
-        g_m = capture(sdm)
-        run(f"[{lay} {n_enc} CUs] encoder alone (masked)", [lambda: encoder(se)])
-        run(f"[{lay} {n_enc} CUs] decode alone on the other {len(db)}", [lambda: decode(g_m, sdm)])
-        run(f"[{lay} {n_enc} CUs] both concurrently (decode on rest)", [lambda: encoder(se), lambda: decode(g_m, sdm)])
-        run(f"[{lay} {n_enc} CUs] both concurrently (decode on full)", [lambda: encoder(se), lambda: decode(g_full, full)])
+plain = torch.cuda.Stream()
+run("encoder (plain stream) + decode (high-priority stream)", [lambda: encoder(plain), lambda: decode(g_hi, hi)])
+for n_enc in (64, 96, 128, 160):
+    se = masked_stream(range(n_enc))
+    run(f"[low {n_enc} CUs] encoder alone (masked)", [lambda: encoder(se)])
+    run(f"[low {n_enc} CUs] both, decode full chip", [lambda: encoder(se), lambda: decode(g_full, full)])
+    run(f"[low {n_enc} CUs] both, decode full chip high priority", [lambda: encoder(se), lambda: decode(g_hi, hi)])
