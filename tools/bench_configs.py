@@ -1,0 +1,159 @@
+#!/usr/bin/env python
+"""BASELINE.json configs 4 and 5 on the MI355X engine (measurement tool beside bench.py, which runs config 3).
+
+config 4  run_pseudo_labelling.py teacher=whisper-large-v3 over a synthetic stand-in for the ReazonSpeech
+          "tiny" shard: 1,768 clips whose durations match misc/data_statistics.json:1 (mean 4.37 s, min
+          0.62 s, max 21.8 s, total 7,723 s), each zero-padded to 30 s; bs 32 per GPU, greedy,
+          return_timestamps=True (the reference default, run_pseudo_labelling.py:99), max_length 128, ja.
+          The data-parallel loop is kwhisper.pseudo_label (accelerate's shard plan, padded all-gather);
+          log-mel on the GPU inside the timed region.  Reports audio-s/s over the REAL durations and over
+          the padded 30 s.
+config 5  kotoba-whisper-v2.0 layout (32 encoder / 2 decoder layers), beam 5 + timestamps, ASR pipeline
+          with chunk_length_s=15 (a 30 s clip -> 3 windows), batch 64 windows.
+
+Random-init weights of each architecture (no checkpoints offline); one JSON line per config on rank 0.
+    python tools/bench_configs.py --config 4 [--n-clips 1768]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_configs.py --config 4
+    python tools/bench_configs.py --config 5 [--clips 64]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kotoba-whisper_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+SR = 16000
+
+
+def reazon_tiny_durations(n: int = 1768, seed: int = 0) -> np.ndarray:
+    """Durations (s) with the shard's statistics (misc/data_statistics.json:1): gamma-shaped, clipped to
+    [0.62, 21.8], rescaled to mean 4.37 s, with the extremes present exactly."""
+    rng = np.random.default_rng(seed)
+    d = rng.gamma(2.2, 4.37 / 2.2, n)
+    for _ in range(20):
+        d = np.clip(d * (4.37 / d.mean()), 0.62, 21.8)
+    d[0], d[1] = 0.62, 21.8
+    d *= (4.37 * n - 0.62 - 21.8) / d[2:].sum() if n > 2 else 1.0
+    d[0], d[1] = 0.62, 21.8
+    return np.clip(d, 0.62, 21.8)
+
+
+def clip_audio(i: int, dur: float) -> np.ndarray:
+    """run_speed_eval.py:14-17 noise, ``dur`` seconds (zero-padded to 30 s by the feature extractor)."""
+    rng = np.random.RandomState(1000 + i)
+    return ((rng.rand(int(dur * SR)) - 0.5) * 2 * 0.007).astype(np.float32)
+
+
+def config4(a, world, rank, dev):
+    from kwhisper.config import PRESETS
+    from kwhisper.feature_extraction import WhisperFeatureExtractor
+    from kwhisper.generation import KWhisperForConditionalGeneration
+    from kwhisper.pseudo_label import pseudo_label
+    from kwhisper.synthetic import synthetic_state_dict_torch
+
+    shape = PRESETS["large-v3"]
+    sd = synthetic_state_dict_torch(shape, seed=0, device=dev)
+    model = KWhisperForConditionalGeneration.from_state_dict(shape, sd, dtype=torch.bfloat16, device=dev)
+    del sd
+    fe = WhisperFeatureExtractor(feature_size=shape.num_mel_bins, device=dev)
+    durs = reazon_tiny_durations()[: a.n_clips]
+    n = len(durs)
+    # the clips live on the host like the reference's dataset; each batch is padded, copied and log-mel'd
+    host = [clip_audio(i, float(d)) for i, d in enumerate(durs)]
+    padded = np.zeros((n, 30 * SR), dtype=np.float32)
+    for i, c in enumerate(host):
+        padded[i, : len(c)] = c
+    pinned = torch.from_numpy(padded).pin_memory()
+
+    def features(idx):
+        return fe.extract(pinned[idx].to(dev, non_blocking=True))
+
+    gen_kw = dict(language="ja", task="transcribe", max_length=a.max_length, return_timestamps=True)
+    # warm-up on one batch (graph capture, workspaces)
+    model.generate(features(list(range(min(a.batch, n)))), **gen_kw)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ids, preds = pseudo_label(model, features, n, batch_size=a.batch, gen_kwargs=gen_kw,
+                              pad_token_id=model.generation_config.pad_token_id)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    assert ids == list(range(n))
+    return {"metric": "audio-seconds/sec pseudo-labelling (real durations)", "value": float(durs.sum()) / dt,
+            "unit": "audio-s/s", "padded_30s_value": n * 30.0 / dt, "n_gpus": world, "clips": n,
+            "audio_seconds": float(durs.sum()), "seconds": dt, "higher_is_better": True, "scaling": "strong",
+            "dtype": "bf16", "data": "synthetic (ReazonSpeech-tiny duration statistics, noise audio, random weights)",
+            "config": {"workload": "config 4: run_pseudo_labelling.py loop, whisper-large-v3, timestamps, greedy",
+                       "per_gpu_batch": a.batch, "max_length": a.max_length, "parallelism": f"dp{world}",
+                       "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))}}
+
+
+def config5(a, dev):
+    from kwhisper.config import PRESETS
+    from kwhisper.generation import KWhisperForConditionalGeneration
+    from kwhisper.pipeline import ASRPipeline
+    from kwhisper.synthetic import synthetic_state_dict_torch
+
+    shape = PRESETS["kotoba-v2.0"]
+    sd = synthetic_state_dict_torch(shape, seed=0, device=dev)
+    model = KWhisperForConditionalGeneration.from_state_dict(shape, sd, dtype=torch.bfloat16, device=dev)
+    del sd
+    pipe = ASRPipeline(model, chunk_length_s=15, batch_size=a.batch,
+                       generate_kwargs=dict(language="ja", task="transcribe", num_beams=5, max_length=a.max_length))
+    clips = [{"array": clip_audio(i, 30.0), "sampling_rate": SR} for i in range(a.clips)]
+    pipe(clips[: max(1, a.batch // 3)], return_timestamps=True)  # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = pipe(clips, return_timestamps=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"metric": "audio-seconds/sec ASR pipeline (chunk 15 s, beam 5, timestamps)",
+            "value": a.clips * 30.0 / dt, "unit": "audio-s/s", "n_gpus": 1, "clips": a.clips, "seconds": dt,
+            "higher_is_better": True, "dtype": "bf16",
+            "data": "synthetic (run_speed_eval.py noise audio, random-init kotoba-whisper-v2.0 layout)",
+            "config": {"workload": "config 5: kotoba-v2.0 (32 enc / 2 dec), beam 5 + timestamps, chunk_length_s 15",
+                       "batch_windows": a.batch, "max_length": a.max_length,
+                       "tokens_per_clip_mean": float(np.mean([len(o["tokens"]) for o in out]))}}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, choices=(4, 5), required=True)
+    ap.add_argument("--n-clips", type=int, default=1768)
+    ap.add_argument("--clips", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--max-length", type=int, default=128)
+    a = ap.parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if a.config == 4:
+        a.batch = a.batch or 32
+        res = config4(a, world, rank, dev)
+    else:
+        a.batch = a.batch or 64
+        res = config5(a, dev)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
