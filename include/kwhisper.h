@@ -193,9 +193,14 @@ typedef struct {
   int32_t* counter;           /* [1] scratch, zero before first use */
   int32_t* n_unfinished;      /* [1] rows still unfinished after this step (written by the last workgroup) */
   float* scores_out;
+  void* workspace;            /* optional, zero-filled once, >= kw_greedy_step_workspace(B) bytes: without
+                                 timestamps / scores_out each row is split over several workgroups whose
+                                 partial argmaxes the row's last arriver combines (NULL: one workgroup per row) */
+  size_t ws_bytes;
 } kw_sampler_args;
 
 int kw_greedy_step(const kw_sampler_args* args, kw_stream_t stream);
+size_t kw_greedy_step_workspace(int64_t B);
 
 /* ---- beam search step (a10: TF/generation/utils.py:3208-3527), num_return_sequences = 1 ----------
  * Running rows are R = B * num_beams, item-major (row = b * num_beams + beam).  One step is

@@ -7,8 +7,9 @@
 // -> finished rows emit pad (:2929) -> MaxLength / EOS stopping (stopping_criteria.py:75-77).
 // The WhisperTimeStamp per-row state (last / penultimate token, last timestamp, finished flag) is
 // derived from the row's own id history each step, exactly as the reference re-derives it from
-// input_ids.  One 1024-thread workgroup per row; the processed row is recomputed on the fly in each
-// of the four L2-resident passes (max, sum, timestamp log-sum-exp, argmax) instead of materialised.
+// input_ids.  With timestamps: one 1024-thread workgroup per row; the processed row is recomputed on
+// the fly in each of the four L2-resident passes (max, sum, timestamp log-sum-exp, argmax) instead of
+// materialised.  Without: greedy_step_split_kernel (a row over NSPLIT workgroups).
 #include <math.h>
 
 #include "processors.h"
@@ -91,13 +92,117 @@ __global__ __launch_bounds__(ST) void greedy_step_kernel(kw_sampler_args a) {
   }
 }
 
+// Split-row variant (no timestamps, no scores_out): row b's V logits are cut into NSPLIT slices of one
+// 512-thread workgroup each (16 loads in flight per thread: one memory round trip per slice instead of
+// a serial walk over the row); each slice publishes its (max, first index) write-through, and the row's
+// last arriver combines the slices in slice order (first index on ties, as torch.argmax) and finishes
+// the step exactly as greedy_step_kernel does.
+constexpr int SPLIT_T = 512, NSPLIT = 8, SUNR = 16;
+
+__global__ __launch_bounds__(SPLIT_T) void greedy_step_split_kernel(kw_sampler_args a) {
+  __shared__ float shf[SPLIT_T / 64];
+  __shared__ int shi[SPLIT_T / 64];
+  const int b = blockIdx.x, sl = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int L = *a.cur_len;
+  const int64_t* ids = a.ids + (int64_t)b * a.ids_stride;
+  const float* x = a.logits + (int64_t)b * a.V;
+  const int V = (int)a.V;
+  const int per = (V + NSPLIT - 1) / NSPLIT;
+  const int v0 = sl * per, v1 = min(V, v0 + per);
+  const bool first = L == a.begin_index;
+  float xv[SUNR];
+#pragma unroll
+  for (int u = 0; u < SUNR; ++u) {
+    const int v = v0 + tid + u * SPLIT_T;
+    xv[u] = v < v1 ? x[v] : -INFINITY;
+  }
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int vb = v0; vb < v1; vb += SPLIT_T * SUNR) {  // one round for V <= NSPLIT * 8192
+    if (vb != v0) {
+#pragma unroll
+      for (int u = 0; u < SUNR; ++u) {
+        const int v = vb + tid + u * SPLIT_T;
+        xv[u] = v < v1 ? x[v] : -INFINITY;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < SUNR; ++u) {
+      const int v = vb + tid + u * SPLIT_T;
+      if (v < v1) {
+        float s = a.suppress_mask[v] ? -INFINITY : xv[u];
+        if (first)
+          for (int i = 0; i < a.n_begin_suppress; ++i)
+            if (a.begin_suppress[i] == v) s = -INFINITY;
+        if (s > best || (s == best && v < bi)) { best = s; bi = v; }
+      }
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  if ((tid & 63) == 0) { shf[tid >> 6] = best; shi[tid >> 6] = bi; }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int i = 1; i < SPLIT_T / 64; ++i)
+    if (shf[i] > best || (shf[i] == best && shi[i] < bi)) { best = shf[i]; bi = shi[i]; }
+  float* part = reinterpret_cast<float*>(a.workspace) + ((int64_t)b * NSPLIT + sl) * 2;
+  int* rcnt = reinterpret_cast<int*>(a.workspace) + (int64_t)a.B * NSPLIT * 2 + b;
+  __hip_atomic_store(part, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(reinterpret_cast<int*>(part) + 1, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int prev = __hip_atomic_fetch_add(rcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (prev != NSPLIT - 1) return;
+  __hip_atomic_store(rcnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const float* row = reinterpret_cast<const float*>(a.workspace) + (int64_t)b * NSPLIT * 2;
+  float bb = -INFINITY;
+  int ii = 0x7fffffff;
+  for (int q = 0; q < NSPLIT; ++q) {  // slice order = index order: strict > keeps the first max
+    const float pv = __hip_atomic_load(row + 2 * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int pi = __hip_atomic_load(reinterpret_cast<const int*>(row) + 2 * q + 1, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    if (pv > bb || (pv == bb && pi < ii)) { bb = pv; ii = pi; }
+  }
+  if (ii == 0x7fffffff) ii = 0;
+  int fin = 0;  // a row is finished once it emitted EOS (stopping_criteria.py:75-77)
+  for (int p = a.begin_index; p < L; ++p) fin |= ids[p] == a.eos_id;
+  const int64_t tok = fin ? (int64_t)a.pad_id : (int64_t)ii;
+  a.ids[(int64_t)b * a.ids_stride + L] = tok;
+  const int done = fin || tok == a.eos_id || (L + 1) >= a.max_length;
+  a.unfinished[b] = done ? 0 : 1;
+  __threadfence();
+  const int prev2 = atomicAdd(a.counter, 1);
+  if (prev2 == (int)a.B - 1) {
+    __threadfence();
+    int n = 0;
+    for (int i = 0; i < (int)a.B; ++i) n += __hip_atomic_load(a.unfinished + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *a.n_unfinished = n;
+    *a.counter = 0;
+    *a.cur_len = L + 1;
+    __threadfence();
+  }
+}
+
 }  // namespace
+
+extern "C" size_t kw_greedy_step_workspace(int64_t B) {
+  return (size_t)B * NSPLIT * 2 * sizeof(float) + (size_t)B * sizeof(int);
+}
 
 extern "C" int kw_greedy_step(const kw_sampler_args* a, kw_stream_t stream) {
   if (!a || !a->logits || !a->suppress_mask || !a->ids || !a->cur_len || !a->unfinished || !a->counter || !a->n_unfinished || a->B <= 0 ||
       a->V <= 0 || (a->n_begin_suppress > 0 && !a->begin_suppress))
     return kw_set_error_msg(KW_EINVAL, "kw_greedy_step: invalid arguments");
-  hipLaunchKernelGGL(greedy_step_kernel, dim3((unsigned)a->B), dim3(ST), 0, (hipStream_t)stream, *a);
+  const bool split = a->workspace && a->ws_bytes >= kw_greedy_step_workspace(a->B) && !a->return_timestamps &&
+                     !a->scores_out;
+  if (split)
+    hipLaunchKernelGGL(greedy_step_split_kernel, dim3((unsigned)a->B, NSPLIT), dim3(SPLIT_T), 0, (hipStream_t)stream, *a);
+  else
+    hipLaunchKernelGGL(greedy_step_kernel, dim3((unsigned)a->B), dim3(ST), 0, (hipStream_t)stream, *a);
   KW_CHECK_LAUNCH();
   return KW_OK;
 }

@@ -60,6 +60,7 @@ class SamplerArgs(ctypes.Structure):
         ("ids", c_vp), ("ids_stride", c_i64),
         ("cur_len", c_vp), ("max_length", c_i32), ("begin_index", c_i32),
         ("unfinished", c_vp), ("counter", c_vp), ("n_unfinished", c_vp), ("scores_out", c_vp),
+        ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
     ]
 
 
@@ -108,6 +109,7 @@ EXPORTS = {
                                           c_vp, ctypes.c_size_t, c_vp]),
     "kw_cross_attn_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64, c_i64]),
     "kw_greedy_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), c_vp]),
+    "kw_greedy_step_workspace": (ctypes.c_size_t, [c_i64]),
     "kw_beam_logprobs": (ctypes.c_int, [ctypes.POINTER(BeamLogprobsArgs), c_vp]),
     "kw_beam_select": (ctypes.c_int, [ctypes.POINTER(BeamSelectArgs), c_vp]),
 }

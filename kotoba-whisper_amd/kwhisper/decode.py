@@ -55,6 +55,8 @@ class DecodeSession:
         self._graph = None
         self._graph_key = None
         self._cross_key = None
+        # split-row sampler partials + per-row arrival counters (zeroed once; kernels leave them zeroed)
+        self.samp_ws = torch.zeros((ops.greedy_step_workspace_bytes(R) + 3) // 4, device=dev, dtype=torch.float32)
         self._greedy_cfg = {}
         self._pinned = None
         if enc is not None:
@@ -237,7 +239,8 @@ class DecodeSession:
                                       return_timestamps=return_timestamps, ts_begin=gen.timestamp_begin,
                                       no_ts_id=gen.no_timestamps_token_id, eos_id=gen.eos_token_id,
                                       pad_id=gen.pad_token_id, max_initial_ts=gen.max_initial_timestamp_index,
-                                      max_length=max_length, begin_index=P, scores_out=score_buf)
+                                      max_length=max_length, begin_index=P, scores_out=score_buf,
+                                      workspace=self.samp_ws)
             cfg = dict(sampler=sampler, score_buf=score_buf, graph=None)
             if len(self._greedy_cfg) >= 8:  # bound the cache (each entry may hold a graph)
                 self._greedy_cfg.pop(next(iter(self._greedy_cfg)))

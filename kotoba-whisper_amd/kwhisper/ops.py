@@ -259,14 +259,20 @@ def cross_attn_step(q, B, q_len, H, hd, k, v, S, out, workspace):
                                       workspace.numel() * workspace.element_size(), _s()), "kw_cross_attn_step")
 
 
+def greedy_step_workspace_bytes(B: int) -> int:
+    return int(_lib().kw_greedy_step_workspace(B))
+
+
 class SamplerPlan:
     """Pre-built ``kw_greedy_step`` call (processors + argmax + stopping on device)."""
 
     def __init__(self, logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, *,
                  return_timestamps, ts_begin, no_ts_id, eos_id, pad_id, max_initial_ts, max_length, begin_index,
-                 scores_out=None):
-        _cuda(logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, scores_out)
-        self._keep = (logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, scores_out)
+                 scores_out=None, workspace=None):
+        _cuda(logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, scores_out,
+              workspace)
+        self._keep = (logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, scores_out,
+                      workspace)
         a = L.SamplerArgs()
         a.logits = logits.data_ptr()
         a.B, a.V = logits.shape
@@ -285,6 +291,8 @@ class SamplerPlan:
         a.counter = counter.data_ptr()
         a.n_unfinished = n_unfinished.data_ptr()
         a.scores_out = scores_out.data_ptr() if scores_out is not None else None
+        a.workspace = workspace.data_ptr() if workspace is not None else None
+        a.ws_bytes = workspace.numel() * workspace.element_size() if workspace is not None else 0
         self.args = a
         self._ref = ctypes.byref(a)
 
