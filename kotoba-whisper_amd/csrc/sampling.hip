@@ -111,6 +111,10 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_kernel(kw_sampler_a
   const int per = (V + NSPLIT - 1) / NSPLIT;
   const int v0 = sl * per, v1 = min(V, v0 + per);
   const bool first = L == a.begin_index;
+  // a row is finished once it emitted EOS (stopping_criteria.py:75-77): one id per thread, in parallel
+  // (the row's last arriver needs it; a serial walk there would pay one load latency per position)
+  int fin = 0;
+  for (int p = a.begin_index + tid; p < L; p += SPLIT_T) fin |= ids[p] == a.eos_id;
   float xv[SUNR];
 #pragma unroll
   for (int u = 0; u < SUNR; ++u) {
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_kernel(kw_sampler_a
     if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
   }
   if ((tid & 63) == 0) { shf[tid >> 6] = best; shi[tid >> 6] = bi; }
-  __syncthreads();
+  fin = __syncthreads_or(fin);
   if (tid != 0) return;
   for (int i = 1; i < SPLIT_T / 64; ++i)
     if (shf[i] > best || (shf[i] == best && shi[i] < bi)) { best = shf[i]; bi = shi[i]; }
@@ -168,8 +172,6 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_kernel(kw_sampler_a
     if (pv > bb || (pv == bb && pi < ii)) { bb = pv; ii = pi; }
   }
   if (ii == 0x7fffffff) ii = 0;
-  int fin = 0;  // a row is finished once it emitted EOS (stopping_criteria.py:75-77)
-  for (int p = a.begin_index; p < L; ++p) fin |= ids[p] == a.eos_id;
   const int64_t tok = fin ? (int64_t)a.pad_id : (int64_t)ii;
   a.ids[(int64_t)b * a.ids_stride + L] = tok;
   const int done = fin || tok == a.eos_id || (L + 1) >= a.max_length;
