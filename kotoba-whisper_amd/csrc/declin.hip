@@ -321,6 +321,137 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
   KW_DEC_STAMP_FLUSH
 }
 
+// LM head (proj_out with the final LayerNorm folded, modeling_whisper.py:790,1080) as a persistent
+// weight stream: the generic kernel above re-reads the 32 activation rows from L2 in every one of its
+// 1,621 workgroups (as many L2 bytes as weight bytes) and runs 1.6 rounds of them.  Here each of
+// ~256 workgroups loads its waves' activation fragments and the rows' LayerNorm statistics ONCE, then
+// walks a contiguous run of column groups (2 x 16 columns each) with the next group's weights in
+// flight while the current one is reduced across waves and written (fixed-order sums: deterministic).
+constexpr int LMH_KTM = 5;   // k-tiles per wave
+constexpr int LMH_NCB = 2;   // column blocks per group
+
+__global__ __launch_bounds__(512) void lm_head_kernel(DecP p, int groups_per_wg) {
+  __shared__ f32x4 red[2][MAXW][LMH_NCB][2][64];  // double-buffered per-wave partial tiles
+  __shared__ float rpart[MAXW][32][2];
+  __shared__ float rstat[32][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int nkt = p.K >> 5;
+  const int kt0 = (nkt * wave) / nw, kt1 = (nkt * (wave + 1)) / nw;  // <= LMH_KTM (host-checked)
+  const int ktl = max(kt1 - 1, kt0);
+  const int M = p.M;
+  const int n_groups = (p.N + 16 * LMH_NCB - 1) / (16 * LMH_NCB);
+  const int g0 = blockIdx.x * groups_per_wg, g1 = min(n_groups, g0 + groups_per_wg);
+  if (g0 >= g1) return;
+  const int n_cb = (p.N + 15) / 16;
+  auto wload = [&](int g, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
+#pragma unroll
+    for (int c = 0; c < LMH_NCB; ++c) {
+      const int cb = min(g * LMH_NCB + c, n_cb - 1);
+#pragma unroll
+      for (int u = 0; u < LMH_KTM; ++u)
+        w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)cb * nkt + min(kt0 + u, ktl)) * 64 + lane);
+    }
+  };
+  bf16x8 wa[LMH_NCB][LMH_KTM], wb[LMH_NCB][LMH_KTM];
+  wload(g0, wa);
+  // activation fragments of this wave's k-range, once (rows lane&15 and 16 + lane&15)
+  bf16x8 a0[LMH_KTM], a1[LMH_KTM];
+  {
+    const int r0 = min(lane & 15, M - 1), r1 = min(16 + (lane & 15), M - 1), akoff = 8 * (lane >> 4);
+#pragma unroll
+    for (int u = 0; u < LMH_KTM; ++u) {
+      const int k = min(kt0 + u, ktl) * 32 + akoff;
+      a0[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r0 * p.ldx + k);
+      a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
+    }
+  }
+  // LayerNorm statistics of the 32 rows on the matrix cores (as dec_linear_kernel step 3)
+  {
+    bf16x8 ones;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+    f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0, q0 = s0, q1 = s0;
+#pragma unroll
+    for (int u = 0; u < LMH_KTM; ++u)
+      if (kt0 + u < kt1) {
+        s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], ones, s0, 0, 0, 0);
+        s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], ones, s1, 0, 0, 0);
+        q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], a0[u], q0, 0, 0, 0);
+        q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], a1[u], q1, 0, 0, 0);
+      }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        rpart[wave][4 * (lane >> 4) + i][0] = s0[i];
+        rpart[wave][16 + 4 * (lane >> 4) + i][0] = s1[i];
+      }
+    }
+    const int di = (lane & 15) - 4 * (lane >> 4);
+    if (di >= 0 && di < 4) {
+      rpart[wave][lane & 15][1] = q0[di];
+      rpart[wave][16 + (lane & 15)][1] = q1[di];
+    }
+    __syncthreads();
+    if (tid < 32) {
+      float sx = 0.f, sq = 0.f;
+      for (int w2 = 0; w2 < nw; ++w2) {
+        sx += rpart[w2][tid][0];
+        sq += rpart[w2][tid][1];
+      }
+      const float inv = 1.f / (float)p.K;
+      const float mean = sx * inv;
+      rstat[tid][0] = mean;
+      rstat[tid][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + p.ln_eps);
+    }
+  }
+  // walk the run: weights of group g+1 in flight while group g is multiplied, reduced and stored
+  auto body = [&](int g, int par, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
+    f32x4 c0[LMH_NCB], c1[LMH_NCB];
+#pragma unroll
+    for (int c = 0; c < LMH_NCB; ++c) {
+      c0[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c1[c] = c0[c];
+#pragma unroll
+      for (int u = 0; u < LMH_KTM; ++u)
+        if (kt0 + u < kt1) {
+          c0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], w[c][u], c0[c], 0, 0, 0);
+          c1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[c][u], c1[c], 0, 0, 0);
+        }
+      red[par][wave][c][0][lane] = c0[c];
+      red[par][wave][c][1][lane] = c1[c];
+    }
+    __syncthreads();  // (double-buffered red: the next group's writes go to the other half)
+    // waves 0..2*NCB-1 each finish one 16 x 16 tile: wave-ordered sum, LayerNorm, bias, store
+    if (wave < 2 * LMH_NCB) {
+      const int c = wave >> 1, hh = wave & 1;
+      f32x4 acc = red[par][0][c][hh][lane];
+      for (int w2 = 1; w2 < nw; ++w2) acc += red[par][w2][c][hh][lane];
+      const int n = (g * LMH_NCB + c) * 16 + (lane & 15);
+      if (n < p.N) {
+        const float cs = p.ln_colsum[n], bn = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * hh + 4 * (lane >> 4) + r;
+          if (m < M) {
+            const float v = rstat[m][1] * (acc[r] - rstat[m][0] * cs) + bn;
+            reinterpret_cast<float*>(p.C)[(int64_t)m * p.ldc + n] = v;
+          }
+        }
+      }
+    }
+  };
+  int par = 0;
+  for (int g = g0; g < g1; g += 2) {
+    if (g + 1 < g1) wload(g + 1, wb);
+    body(g, par, wa);
+    par ^= 1;
+    if (g + 1 >= g1) break;
+    if (g + 2 < g1) wload(g + 2, wa);
+    body(g + 1, par, wb);
+    par ^= 1;
+  }
+}
+
 __global__ void pack_kernel(const bf16_t* __restrict__ W, int N, int K, bf16_t* __restrict__ out) {
   const int nkt = K >> 5;
   const int64_t total = (int64_t)((N + 31) / 32 * 2) * nkt * 64;
@@ -436,6 +567,9 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
       return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: needs a zero-filled workspace of kw_dec_linear_workspace_bytes()");
   }
   hipStream_t s = (hipStream_t)stream;
+  // LM head: LayerNorm-fused, f32 logits, a wide N and a short K -> the persistent weight stream
+  const bool lmh = a->ln && a->epilogue == KW_EPI_STORE && a->c_dtype == KW_DT_F32 && a->N >= 8192 &&
+                   (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && !a->gelu && a->scale_cols == 0;
   for (int64_t m0 = 0; m0 < a->M; m0 += 32) {  // 32-row chunks (weights re-streamed per chunk)
     DecP p;
     p.M = (int)(a->M - m0 < 32 ? a->M - m0 : 32);
@@ -460,6 +594,23 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     p.cnt = reinterpret_cast<int*>(a->workspace);
     p.slab = a->workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(a->workspace) + CNT_MAX * sizeof(int)) : nullptr;
     p.xlds = use_xlds(a->N, g) ? 1 : 0;
+    if (lmh) {
+      static int ncu = 0;
+      if (!ncu) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            ncu <= 0)
+          ncu = 256;
+      }
+      const int groups = (int)((a->N + 16 * LMH_NCB - 1) / (16 * LMH_NCB));
+      const int per = (groups + ncu - 1) / ncu;
+      const int nwv = (nkt + LMH_KTM - 1) / LMH_KTM;
+      hipLaunchKernelGGL(lm_head_kernel, dim3((unsigned)((groups + per - 1) / per)), dim3((unsigned)(64 * nwv)), 0, s, p,
+                         per);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return kw_set_error(e);
+      continue;
+    }
     hipError_t e = launch(p, a->epilogue == KW_EPI_RESID, g, a->c_dtype == KW_DT_F32, s);
     if (e != hipSuccess) return kw_set_error(e);
   }
