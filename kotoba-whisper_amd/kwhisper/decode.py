@@ -247,9 +247,27 @@ class DecodeSession:
             self._greedy_cfg[key] = cfg
         sampler, score_buf = cfg["sampler"], cfg["score_buf"]
         self.scores = [] if record_scores else None
-        # prefill
-        self._run(self._step_plans(P))
-        sampler()
+        # prefill (replayed from a graph cached with the configuration: ~260 launches otherwise go
+        # through Python one by one)
+        def prefill():
+            self._run(self._step_plans(P))
+            sampler()
+
+        pg = cfg.get("prefill_graph")
+        if pg is None and use_graph and not record_scores:
+            pg = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.graph(pg, stream=side):
+                prefill()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            cfg["prefill_graph"] = pg
+            # capture only records: the kernels have not run yet, and the state the prefill consumes
+            # (ids, cur_len, counters) is untouched -- replay below
+        if pg is not None and use_graph and not record_scores:
+            pg.replay()
+        else:
+            prefill()
         if record_scores:
             self.scores.append((self.logits.clone(), score_buf.clone()))
         n_steps = max_length - P  # tokens the reference can add at most
@@ -319,50 +337,87 @@ class DecodeSession:
         self.ids[:, :P].copy_(prompt.to(dev).repeat_interleave(nb, 0))
         self.cur_len.fill_(P)
         self.bp.copy_(torch.arange(R, device=dev, dtype=torch.int32)[:, None].expand(R, T_MAX))
-        run = torch.zeros((B, nb), device=dev, dtype=torch.float32)
-        run[:, 1:] = -1.0e9
-        st = dict(
-            ids=self.ids, bp=self.bp, cur_len=self.cur_len, run_scores=run.view(-1),
-            fin_seq=torch.full((B, nb, max_length), fill, device=dev, dtype=torch.int64),
-            fin_score=torch.full((B, nb), -1.0e9, device=dev, dtype=torch.float32),
-            fin_len=torch.zeros((B, nb), device=dev, dtype=torch.int32),
-            fin_flag=torch.zeros((B, nb), device=dev, dtype=torch.int32),
-            unsat=torch.ones((B,), device=dev, dtype=torch.int32),
-            counter=torch.zeros((1,), device=dev, dtype=torch.int32),
-            go=torch.ones((1,), device=dev, dtype=torch.int32),
-            done=torch.zeros((1,), device=dev, dtype=torch.int32),
-            item_flags=torch.zeros((B, 3), device=dev, dtype=torch.int32),
-            cand_val=torch.empty((R, 2 * nb), device=dev, dtype=torch.float32),
-            cand_idx=torch.empty((R, 2 * nb), device=dev, dtype=torch.int32),
-        )
-        sup = torch.zeros((V,), dtype=torch.uint8)
-        if gen.suppress_tokens:
-            sup[torch.tensor(gen.suppress_tokens)] = 1
-        self._sup = sup.to(dev)
-        bsup = torch.tensor(gen.begin_suppress_tokens or [0], dtype=torch.int32, device=dev)
-        step = ops.BeamStepPlan(st, self.logits, self._sup, bsup if gen.begin_suppress_tokens else None,
-                                return_timestamps=return_timestamps, ts_begin=gen.timestamp_begin,
-                                no_ts_id=gen.no_timestamps_token_id, eos_id=gen.eos_token_id,
-                                max_initial_ts=gen.max_initial_timestamp_index, begin_index=P, max_length=max_length,
-                                fill_id=fill, length_penalty=length_penalty, early_stopping=early_stopping)
+        # beam state, step plan and captured graphs are kept per configuration and re-initialised in
+        # place, so a repeat call replays the same graphs (no re-capture, see generate)
+        key = ("beam", max_length, P, bool(return_timestamps), float(length_penalty), str(early_stopping), fill,
+               tuple(gen.suppress_tokens or ()), tuple(gen.begin_suppress_tokens or ()), gen.timestamp_begin,
+               gen.no_timestamps_token_id, gen.eos_token_id, gen.max_initial_timestamp_index)
+        cfg = self._greedy_cfg.get(key)
+        if cfg is None:
+            st = dict(
+                ids=self.ids, bp=self.bp, cur_len=self.cur_len,
+                run_scores=torch.empty((B * nb,), device=dev, dtype=torch.float32),
+                fin_seq=torch.empty((B, nb, max_length), device=dev, dtype=torch.int64),
+                fin_score=torch.empty((B, nb), device=dev, dtype=torch.float32),
+                fin_len=torch.empty((B, nb), device=dev, dtype=torch.int32),
+                fin_flag=torch.empty((B, nb), device=dev, dtype=torch.int32),
+                unsat=torch.empty((B,), device=dev, dtype=torch.int32),
+                counter=torch.zeros((1,), device=dev, dtype=torch.int32),
+                go=torch.empty((1,), device=dev, dtype=torch.int32),
+                done=torch.empty((1,), device=dev, dtype=torch.int32),
+                item_flags=torch.empty((B, 3), device=dev, dtype=torch.int32),
+                cand_val=torch.empty((R, 2 * nb), device=dev, dtype=torch.float32),
+                cand_idx=torch.empty((R, 2 * nb), device=dev, dtype=torch.int32),
+            )
+            sup = torch.zeros((V,), dtype=torch.uint8)
+            if gen.suppress_tokens:
+                sup[torch.tensor(gen.suppress_tokens)] = 1
+            sup = sup.to(dev)
+            bsup = torch.tensor(gen.begin_suppress_tokens or [0], dtype=torch.int32, device=dev)
+            step = ops.BeamStepPlan(st, self.logits, sup, bsup if gen.begin_suppress_tokens else None,
+                                    return_timestamps=return_timestamps, ts_begin=gen.timestamp_begin,
+                                    no_ts_id=gen.no_timestamps_token_id, eos_id=gen.eos_token_id,
+                                    max_initial_ts=gen.max_initial_timestamp_index, begin_index=P,
+                                    max_length=max_length, fill_id=fill, length_penalty=length_penalty,
+                                    early_stopping=early_stopping)
+            cfg = dict(st=st, step=step, graph=None, prefill_graph=None)
+            if len(self._greedy_cfg) >= 8:
+                self._greedy_cfg.pop(next(iter(self._greedy_cfg)))
+            self._greedy_cfg[key] = cfg
+        st, step = cfg["st"], cfg["step"]
+        st["run_scores"].view(B, nb).fill_(-1.0e9)
+        st["run_scores"].view(B, nb)[:, 0] = 0.0
+        st["fin_seq"].fill_(fill)
+        st["fin_score"].fill_(-1.0e9)
+        st["fin_len"].zero_()
+        st["fin_flag"].zero_()
+        st["unsat"].fill_(1)
+        st["counter"].zero_()
+        st["go"].fill_(1)
+        st["done"].zero_()
+        st["item_flags"].zero_()
         self._beam_state = st
-        self._run(self._step_plans(P))  # prefill on every running row (the reference expands x num_beams)
-        step()
+
+        def prefill():
+            self._run(self._step_plans(P))  # prefill on every running row (the reference expands x num_beams)
+            step()
+
         step_seq = self._step_plans(1)
 
         def one_step():
             self._run(step_seq)
             step()
 
-        graph = None
+        def captured(name, fn):
+            g = cfg[name]
+            if g is None:
+                g = torch.cuda.CUDAGraph()
+                side = torch.cuda.Stream(device=dev)
+                side.wait_stream(torch.cuda.current_stream(dev))
+                with torch.cuda.graph(g, stream=side):
+                    fn()
+                torch.cuda.current_stream(dev).wait_stream(side)
+                cfg[name] = g
+            return g
+
         if use_graph:
-            graph = torch.cuda.CUDAGraph()
-            side = torch.cuda.Stream(device=dev)
-            side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.graph(graph, stream=side):
-                one_step()
-            torch.cuda.current_stream(dev).wait_stream(side)
-        pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
+            captured("prefill_graph", prefill).replay()
+        else:
+            prefill()
+        graph = captured("graph", one_step) if use_graph else None
+        if self._pinned is None or self._pinned.numel() < check_every + 1:
+            self._pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
+        pinned = self._pinned
         events = []
         n = 1
         while n < max_length - P + 1:
