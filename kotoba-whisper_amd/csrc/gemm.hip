@@ -309,7 +309,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
   prologue();
   prologue_wait(false);
 
-  int tcount = 0;
+  [[maybe_unused]] int tcount = 0;  // tile counter for the lab stamps
   KW_GEMM_STAMP(0);
   for (;;) {
     // an opaque copy of the lane id per tile: keeps the epilogue's lane-derived addresses from being

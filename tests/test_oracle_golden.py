@@ -115,6 +115,9 @@ def test_oracle_large_generate(gold, shape, tag):
     feats = oracle_features(shape, g["cases"])
     enc = model.encode(feats)
     np.testing.assert_allclose(enc[:, ::50, :], g["enc_slice"], atol=5e-4, rtol=1e-3)
+    # generate re-encodes the same mel: serve it from the pass above (the numpy large encoder is minutes)
+    encode, key = model.encode, feats.tobytes()
+    model.encode = lambda x: enc if x.tobytes() == key else encode(x)
     toks = og.generate(model, feats, gen_dict(shape), max_length=int(g["max_length"]), language="ja",
                        task="transcribe", return_timestamps=False)
     np.testing.assert_array_equal(toks, g["greedy_tokens"])
