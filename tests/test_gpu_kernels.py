@@ -366,6 +366,29 @@ def test_cross_attn_step(dtype, q_len, S):
     torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
 
 
+@pytest.mark.parametrize("q_len", [2, 4, 5, 20])
+@pytest.mark.parametrize("S", [1500, 200])
+def test_cross_attn_multirow_bitwise(q_len, S):
+    """bf16 rows of one item sharing a K/V pass (prefill positions, beams) == each row attended alone by
+    the one-row kernel, bit for bit."""
+    B, H, hd = 3, 20, 64
+    d = H * hd
+    dtype = torch.bfloat16
+    k = torch.randn(B, H, S, hd, device="cuda").to(dtype)
+    v = torch.randn(B, H, S, hd, device="cuda").to(dtype)
+    q = (torch.randn(B * q_len, d, device="cuda") * 0.3).to(dtype)
+    out = torch.empty(B * q_len, d, device="cuda", dtype=dtype)
+    ws = torch.zeros(ops.cross_attn_workspace_bytes(B, q_len, H, hd, S) // 4 + 1, device="cuda")
+    for _ in range(2):
+        ops.cross_attn_step(q, B, q_len, H, hd, k, v, S, out, ws)
+    one = torch.empty(B, d, device="cuda", dtype=dtype)
+    ws1 = torch.zeros(ops.cross_attn_workspace_bytes(B, 1, H, hd, S) // 4 + 1, device="cuda")
+    qv = q.view(B, q_len, d)
+    for i in range(q_len):
+        ops.cross_attn_step(qv[:, i].contiguous(), B, 1, H, hd, k, v, S, one, ws1)
+        assert torch.equal(out.view(B, q_len, d)[:, i], one), i
+
+
 # ---------------------------------------------------------------- greedy step (processors + argmax)
 def _random_history(rng, B, P, n, ts_begin, V, eos, pad):
     ids = np.zeros((B, P + n), np.int64)
