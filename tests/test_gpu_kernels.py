@@ -445,23 +445,28 @@ def test_greedy_step_vs_oracle(rt, n_hist):
     assert int(nun.item()) == int(unf.sum().item())
 
 
+@pytest.mark.parametrize("rt", [False, True])
 @pytest.mark.parametrize("n_hist", [0, 1, 7])
 @pytest.mark.parametrize("B,V", [(32, 51866), (6, 51865), (3, 1000), (2, 9)])
-def test_greedy_step_split_rows(n_hist, B, V):
-    """Split-row sampler (no timestamps; a row over 8 workgroups + last-arriver combine) == the one-workgroup
-    kernel, token for token, including ties (first index wins), EOS-finished rows, the begin-suppress
-    step and the cur_len / n_unfinished bookkeeping, over repeated steps (counters left zeroed)."""
+def test_greedy_step_split_rows(rt, n_hist, B, V):
+    """Split-row sampler (a row over 8 workgroups + last-arriver combine; with timestamps the probability-mass
+    rule from merged per-slice log-sum-exps) == the one-workgroup kernel, token for token: ties (first
+    index wins), EOS-finished rows, the begin-suppress step, timestamp pairing / monotonicity / initial
+    rules, the text ban, and the cur_len / n_unfinished bookkeeping over repeated steps."""
     from kwhisper.config import LARGE_V3, generation_constants
 
     gen = generation_constants(LARGE_V3)
     P = 3
-    rng = np.random.default_rng(1000 * n_hist + V + B)
-    eos = min(gen.eos_token_id, V - 1)
-    hist = rng.integers(0, V, (B, P + n_hist))
+    rng = np.random.default_rng(1000 * n_hist + V + B + 7 * rt)
+    eos = min(gen.eos_token_id, V - 4)
+    ts_begin = gen.timestamp_begin if V > gen.timestamp_begin else V - 3
+    no_ts = ts_begin - 1
+    hist = rng.integers(0, eos, (B, P + n_hist))
     if n_hist:
         hist[0, P] = eos  # a finished row
+        hist[1 % B, P:] = rng.integers(ts_begin, V, n_hist)  # a row of timestamps
     sup = torch.zeros(V, dtype=torch.uint8)
-    sup[torch.tensor([t for t in gen.suppress_tokens if t < V][:50] + [1])] = 1
+    sup[torch.tensor([t for t in gen.suppress_tokens if t < no_ts][:50] + [1])] = 1
     bsup = torch.tensor([0, min(220, V - 1)], dtype=torch.int32, device="cuda")
     outs = []
     for split in (False, True):
@@ -473,18 +478,23 @@ def test_greedy_step_split_rows(n_hist, B, V):
         nun = torch.zeros(1, dtype=torch.int32, device="cuda")
         lg = torch.empty((B, V), device="cuda")
         ws = torch.zeros(ops.greedy_step_workspace_bytes(B) // 4 + 1, device="cuda") if split else None
-        plan = ops.SamplerPlan(lg, sup.cuda(), bsup, ids, cur, unf, cnt, nun, return_timestamps=False,
-                               ts_begin=V, no_ts_id=V - 1, eos_id=eos, pad_id=gen.pad_token_id % V,
-                               max_initial_ts=None, max_length=hist.shape[1] + 5, begin_index=P, workspace=ws)
+        plan = ops.SamplerPlan(lg, sup.cuda(), bsup, ids, cur, unf, cnt, nun, return_timestamps=rt,
+                               ts_begin=ts_begin, no_ts_id=no_ts, eos_id=eos, pad_id=gen.pad_token_id % V,
+                               max_initial_ts=50 if rt else None, max_length=hist.shape[1] + 5, begin_index=P,
+                               workspace=ws)
         srng = np.random.default_rng(7)
-        for _ in range(4):
-            x = srng.integers(-3, 4, (B, V)).astype(np.float32)  # many ties
+        for step in range(4):
+            if rt:  # continuous scores (no exact ties between the log-sum-exp sides), some rows favour stamps
+                x = (srng.standard_normal((B, V)) * 3).astype(np.float32)
+                x[::2, ts_begin:] += 4.0 + step
+            else:
+                x = srng.integers(-3, 4, (B, V)).astype(np.float32)  # many ties
             lg.copy_(torch.from_numpy(x))
             plan()
         torch.cuda.synchronize()
         outs.append((ids.cpu().numpy(), int(cur.item()), unf.cpu().numpy(), int(nun.item()), int(cnt.item())))
         if split:
-            assert not ws.view(torch.int32)[B * 16: B * 17].any()  # per-row counters back at zero
+            assert not ws.view(torch.int32)[B * 64: B * 65].any()  # per-row counters back at zero
     (a_ids, a_cur, a_unf, a_nun, a_cnt), (b_ids, b_cur, b_unf, b_nun, b_cnt) = outs
     np.testing.assert_array_equal(a_ids, b_ids)
     assert (a_cur, a_nun, a_cnt) == (b_cur, b_nun, b_cnt) and (a_unf == b_unf).all()
