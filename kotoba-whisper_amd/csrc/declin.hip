@@ -43,6 +43,7 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_base) {
 constexpr int CNT_MAX = 4096;  // seam arrival counters at the start of the workspace
 constexpr int MAXW = 8;        // waves per workgroup
 constexpr int KSMAX = 8;       // K splits per column group (host-checked)
+constexpr int ZMAX = 8;        // 32-row chunks per K-split launch (workspace sized for them)
 
 struct DecP {
   const bf16_t* x;
@@ -67,7 +68,24 @@ struct DecP {
 };
 
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
-__global__ __launch_bounds__(512) void dec_linear_kernel(DecP p, int ksn) {
+__global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
+  // blockIdx.z = 32-row chunk: a launch covers M rows as independent 32-row tiles (their workgroups
+  // run concurrently and the repeat weight reads of the later chunks hit the caches)
+  DecP p = p0;
+  if (ksn > 1) {  // K-split seam: each chunk has its own counters and partial slabs
+    p.cnt += blockIdx.z * gridDim.x;
+    p.slab += (int64_t)blockIdx.z * gridDim.x * ksn * (NCB * 512);
+  }
+  if (blockIdx.z) {
+    const int m0 = 32 * blockIdx.z;
+    p.M = min(32, p0.M - m0);
+    p.x += m0 * p0.ldx;
+    if (p.C) p.C = reinterpret_cast<char*>(p.C) + (int64_t)m0 * p0.ldc * (sizeof(TC));
+    if (p.h) p.h += m0 * p0.ldh;
+    if (p.hb) p.hb += m0 * p0.ldh;
+  } else {
+    p.M = min(32, p0.M);
+  }
   __shared__ f32x4 red[MAXW][NCB][2][64];
   __shared__ float rpart[MAXW][32][2];  // LayerNorm: per-wave row (sum, sum of squares)
   __shared__ float rstat[32][2];     // LayerNorm: (mean, rstd) per row
@@ -513,7 +531,7 @@ hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = shm;
   }
-  const dim3 grid((unsigned)((p.N + 16 * NCB - 1) / (16 * NCB)), (unsigned)g.ks);
+  const dim3 grid((unsigned)((p.N + 16 * NCB - 1) / (16 * NCB)), (unsigned)g.ks, (unsigned)((p.M + 31) / 32));
   const dim3 block((unsigned)(64 * g.nw));
   hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, EPI, TC>), grid, block, shm, s, p, g.ks);
   return hipGetLastError();
@@ -537,7 +555,7 @@ hipError_t launch(const DecP& p, bool resid, const Geo& g, bool c_f32, hipStream
 extern "C" size_t kw_dec_linear_workspace_bytes(int64_t N, int64_t K) {
   const Geo g = choose(N, K);
   const int64_t ncg = (N + 16 * g.ncb - 1) / (16 * g.ncb);
-  return (size_t)CNT_MAX * sizeof(int) + (g.ks > 1 ? (size_t)ncg * g.ks * g.ncb * 512 * sizeof(float) : 0);
+  return (size_t)CNT_MAX * sizeof(int) + (g.ks > 1 ? (size_t)ZMAX * ncg * g.ks * g.ncb * 512 * sizeof(float) : 0);
 }
 
 extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
@@ -562,7 +580,7 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_linear: K too long for the k-tile budget");
   const int64_t ncg = (a->N + 16 * g.ncb - 1) / (16 * g.ncb);
   if (g.ks > 1) {
-    if (ncg > CNT_MAX) return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: split-K needs N <= 65536");
+    if (ncg * ZMAX > CNT_MAX) return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: split-K needs N <= 8192");
     if (!a->workspace || a->ws_bytes < kw_dec_linear_workspace_bytes(a->N, a->K))
       return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: needs a zero-filled workspace of kw_dec_linear_workspace_bytes()");
   }
@@ -570,9 +588,12 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
   // LM head: LayerNorm-fused, f32 logits, a wide N and a short K -> the persistent weight stream
   const bool lmh = a->ln && a->epilogue == KW_EPI_STORE && a->c_dtype == KW_DT_F32 && a->N >= 8192 &&
                    (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && !a->gelu && a->scale_cols == 0;
-  for (int64_t m0 = 0; m0 < a->M; m0 += 32) {  // 32-row chunks (weights re-streamed per chunk)
+  // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each);
+  // the LM head loops over chunks
+  const int64_t step = lmh ? 32 : g.ks == 1 ? a->M : 32 * ZMAX;
+  for (int64_t m0 = 0; m0 < a->M; m0 += step) {
     DecP p;
-    p.M = (int)(a->M - m0 < 32 ? a->M - m0 : 32);
+    p.M = (int)(a->M - m0 < step ? a->M - m0 : step);
     p.N = (int)a->N;
     p.K = (int)a->K;
     p.x = reinterpret_cast<const bf16_t*>(a->x) + m0 * a->ldx;

@@ -519,7 +519,7 @@ def test_dec_linear_layernorm(M, N, K):
     torch.testing.assert_close(C, _ref_gemm(xn, W, bias), atol=4e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("M", [32, 5, 70])
+@pytest.mark.parametrize("M", [32, 5, 70, 300])
 @pytest.mark.parametrize("N,K", [(1280, 1280), (1280, 5120), (384, 1536)])
 def test_dec_linear_resid(M, N, K):
     """RESID epilogue (h += x W^T + b, bf16 mirror); K 5120 exercises the K-split seam.  Run twice:
