@@ -348,7 +348,11 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
 constexpr int LMH_KTM = 5;   // k-tiles per wave
 constexpr int LMH_NCB = 2;   // column blocks per group
 
-__global__ __launch_bounds__(512) void lm_head_kernel(DecP p, int groups_per_wg) {
+__global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg) {
+  DecP p = p0;  // blockIdx.z = 32-row chunk (beam rows), as in dec_linear_kernel
+  p.M = min(32, p0.M - 32 * (int)blockIdx.z);
+  p.x += (int64_t)32 * blockIdx.z * p0.ldx;
+  p.C = reinterpret_cast<float*>(p0.C) + (int64_t)32 * blockIdx.z * p0.ldc;
   __shared__ f32x4 red[2][MAXW][LMH_NCB][2][64];  // double-buffered per-wave partial tiles
   __shared__ float rpart[MAXW][32][2];
   __shared__ float rstat[32][2];
@@ -588,9 +592,8 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
   // LM head: LayerNorm-fused, f32 logits, a wide N and a short K -> the persistent weight stream
   const bool lmh = a->ln && a->epilogue == KW_EPI_STORE && a->c_dtype == KW_DT_F32 && a->N >= 8192 &&
                    (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && !a->gelu && a->scale_cols == 0;
-  // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each);
-  // the LM head loops over chunks
-  const int64_t step = lmh ? 32 : g.ks == 1 ? a->M : 32 * ZMAX;
+  // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each)
+  const int64_t step = (g.ks == 1 || lmh) ? a->M : 32 * ZMAX;
   for (int64_t m0 = 0; m0 < a->M; m0 += step) {
     DecP p;
     p.M = (int)(a->M - m0 < step ? a->M - m0 : step);
@@ -626,8 +629,8 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
       const int groups = (int)((a->N + 16 * LMH_NCB - 1) / (16 * LMH_NCB));
       const int per = (groups + ncu - 1) / ncu;
       const int nwv = (nkt + LMH_KTM - 1) / LMH_KTM;
-      hipLaunchKernelGGL(lm_head_kernel, dim3((unsigned)((groups + per - 1) / per)), dim3((unsigned)(64 * nwv)), 0, s, p,
-                         per);
+      hipLaunchKernelGGL(lm_head_kernel, dim3((unsigned)((groups + per - 1) / per), 1, (unsigned)((p.M + 31) / 32)),
+                         dim3((unsigned)(64 * nwv)), 0, s, p, per);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return kw_set_error(e);
       continue;
