@@ -227,9 +227,13 @@ typedef struct {
   float* cand_val;
   int32_t* cand_idx;
   const int32_t* done;
+  void* workspace;            /* optional, zero-filled once, >= kw_beam_logprobs_workspace(R) bytes: each row
+                                 over several workgroups + a last-arriver merge (NULL: one workgroup per row) */
+  size_t ws_bytes;
 } kw_beam_logprobs_args;
 
 int kw_beam_logprobs(const kw_beam_logprobs_args* args, kw_stream_t stream);
+size_t kw_beam_logprobs_workspace(int64_t R);
 
 /* Selection for one step (utils.py:3077-3205, 3008-3075): top 2*num_beams continuations over
  * beams x vocab of (log-prob + running score), MaxLength / EOS criteria, the next running beams

@@ -133,6 +133,241 @@ __global__ __launch_bounds__(ST) void beam_logprobs_kernel(kw_beam_logprobs_args
   }
 }
 
+// ---- split-row variant: a row over BSPLIT workgroups (the one-workgroup kernel above walks a whole
+// vocabulary row serially in several passes; at R = 160-320 running rows that is most of a step).
+// Each slice keeps its logits in registers and publishes: the raw maximum and sum of exp (the
+// log_softmax normaliser), WhisperTimeStamp's statistics of its processed scores (as the greedy
+// split kernel), and its best KP processed scores overall and among timestamps (KP = k + 4 > k, so a
+// log-prob tie that the raw order would split differently stays inside the candidates).  The row's
+// last arriver merges the normaliser, applies the timestamp rule, turns candidates into log-probs
+// lp = (x - m) - log(s) and keeps the k best by (lp desc, token asc).
+constexpr int BSPLIT = 8, BT_S = 512, BUNR = 16, KP = KMAX + 4, BPART = 96;
+
+__device__ __forceinline__ void bl_argmax(float& best, int& bi, int& bt, float* shf, int* shi) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64), ot = __shfl_xor(bt, o, 64);
+    if (better(ob, oi, best, bi)) { best = ob; bi = oi; bt = ot; }
+  }
+  if ((threadIdx.x & 63) == 0) {
+    shf[threadIdx.x >> 6] = best;
+    shi[2 * (threadIdx.x >> 6)] = bi;
+    shi[2 * (threadIdx.x >> 6) + 1] = bt;
+  }
+  __syncthreads();
+  best = shf[0]; bi = shi[0]; bt = shi[1];
+  for (int w = 1; w < BT_S / 64; ++w)
+    if (better(shf[w], shi[2 * w], best, bi)) { best = shf[w]; bi = shi[2 * w]; bt = shi[2 * w + 1]; }
+  __syncthreads();
+}
+__device__ __forceinline__ float bl_max(float v, float* sh) {
+  v = wave_max(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = sh[0];
+  for (int i = 1; i < BT_S / 64; ++i) r = fmaxf(r, sh[i]);
+  __syncthreads();
+  return r;
+}
+__device__ __forceinline__ float bl_sum(float v, float* sh) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < BT_S / 64; ++i) r += sh[i];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logprobs_args a) {
+  __shared__ float shf[BT_S / 64];
+  __shared__ int shi[2 * (BT_S / 64)];
+  __shared__ RowState st_sh;
+  __shared__ float pub[BPART];
+  if (*a.done) return;
+  const int r = blockIdx.x, sl = blockIdx.y;
+  const int tid = threadIdx.x;
+  const int L = *a.cur_len;
+  const int V = (int)a.V;
+  const int K = a.k;
+  const float* x = a.logits + (int64_t)r * a.V;
+  const int64_t* ids = a.ids + (int64_t)r * a.ids_stride;
+  const int per = (V + BSPLIT - 1) / BSPLIT;
+  const int v0 = sl * per, v1 = min(V, v0 + per);
+  float xv[BUNR];
+#pragma unroll
+  for (int u = 0; u < BUNR; ++u) {
+    const int v = v0 + tid + u * BT_S;
+    xv[u] = v < v1 ? x[v] : -INFINITY;
+  }
+  // row state from the history (as kwp::row_state, BT_S threads)
+  int lsp = -1;
+  for (int p = a.begin_index + tid; p < L; p += BT_S)
+    if (ids[p] >= a.ts_begin) lsp = max(lsp, p);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lsp = max(lsp, __shfl_xor(lsp, o, 64));
+  if ((tid & 63) == 0) shi[tid >> 6] = lsp;
+  __syncthreads();
+  if (tid == 0) {
+    int lp = shi[0];
+    for (int i = 1; i < BT_S / 64; ++i) lp = max(lp, shi[i]);
+    RowState st;
+    st.L = L; st.begin = a.begin_index; st.ts_begin = a.ts_begin; st.no_ts = a.no_ts_id; st.eos = a.eos_id;
+    st.rt = a.return_timestamps; st.max_init = a.max_initial_ts; st.ban_text = 0;
+    const int n = L - a.begin_index;
+    st.first_step = (L == a.begin_index);
+    st.last_ts = n >= 1 && ids[L - 1] >= a.ts_begin;
+    st.pen_ts = n < 2 || ids[L - 2] >= a.ts_begin;
+    st.has_stamp = lp >= 0;
+    st.stamp_lo = st.has_stamp ? ((st.last_ts && !st.pen_ts) ? (int)ids[lp] : (int)ids[lp] + 1) : 0;
+    st_sh = st;
+  }
+  __syncthreads();
+  const RowState st = st_sh;
+  // log_softmax normaliser pieces over the RAW slice
+  float mr = -INFINITY;
+#pragma unroll
+  for (int u = 0; u < BUNR; ++u) mr = fmaxf(mr, xv[u]);
+  mr = bl_max(mr, shf);
+  float sr = 0.f;
+#pragma unroll
+  for (int u = 0; u < BUNR; ++u)
+    if (v0 + tid + u * BT_S < v1) sr += expf(xv[u] - mr);
+  sr = bl_sum(sr, shf);
+  // processed scores (raw-logit space; every processor is shift invariant) and their statistics
+  float sv[BUNR];
+  float mt = -INFINITY, ms = -INFINITY;
+  int it = 0x7fffffff, is = 0x7fffffff, dummy = 0;
+#pragma unroll
+  for (int u = 0; u < BUNR; ++u) {
+    const int v = v0 + tid + u * BT_S;
+    sv[u] = v < v1 ? process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, xv[u]) : -INFINITY;
+    if (v < v1) {
+      if (v < st.ts_begin) {
+        if (better(sv[u], v, mt, it)) { mt = sv[u]; it = v; }
+      } else if (better(sv[u], v, ms, is)) { ms = sv[u]; is = v; }
+    }
+  }
+  float sa = 0.f, sts = 0.f, mall = -INFINITY;
+  if (st.rt) {
+    bl_argmax(mt, it, dummy, shf, shi);
+    bl_argmax(ms, is, dummy, shf, shi);
+    mall = fmaxf(mt, ms);
+    if (mall > -INFINITY) {
+#pragma unroll
+      for (int u = 0; u < BUNR; ++u) {
+        const int v = v0 + tid + u * BT_S;
+        if (v < v1 && sv[u] > -INFINITY) {
+          sa += expf(sv[u] - mall);
+          if (v >= st.ts_begin) sts += expf(sv[u] - ms);
+        }
+      }
+    }
+    sa = bl_sum(sa, shf);
+    sts = bl_sum(sts, shf);
+  }
+  // the slice's KP best processed scores (all tokens; and timestamps only, for the text-ban case)
+  const int kp = min(K + 4, KP);
+  for (int list = 0; list < (st.rt ? 2 : 1); ++list) {
+    unsigned taken = 0;
+    for (int j = 0; j < kp; ++j) {
+      float bv = -INFINITY;
+      int bi = 0x7fffffff, bu = -1;
+#pragma unroll
+      for (int u = 0; u < BUNR; ++u) {
+        const int v = v0 + tid + u * BT_S;
+        if (v < v1 && !(taken >> u & 1) && (list == 0 || v >= st.ts_begin) && better(sv[u], v, bv, bi)) {
+          bv = sv[u]; bi = v; bu = u;
+        }
+      }
+      int bt = tid;
+      bl_argmax(bv, bi, bt, shf, shi);
+      if (tid == bt && bu >= 0 && bi == v0 + tid + bu * BT_S) taken |= 1u << bu;
+      if (tid == 0) {
+        pub[9 + list * 2 * KP + 2 * j] = bv;
+        pub[9 + list * 2 * KP + 2 * j + 1] = __int_as_float(bi);
+      }
+    }
+  }
+  if (tid == 0) {
+    pub[0] = mr; pub[1] = sr; pub[2] = mt; pub[3] = __int_as_float(it); pub[4] = ms;
+    pub[5] = __int_as_float(is); pub[6] = mall; pub[7] = sa; pub[8] = sts;
+  }
+  __syncthreads();
+  float* part = reinterpret_cast<float*>(a.workspace) + ((int64_t)r * BSPLIT + sl) * BPART;
+  int* rcnt = reinterpret_cast<int*>(a.workspace) + (int64_t)a.R * BSPLIT * BPART + r;
+  const int npub = 9 + (st.rt ? 4 : 2) * KP;
+  if (tid < npub) __hip_atomic_store(part + tid, pub[tid], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int last;
+  if (tid == 0) {
+    const int prev = __hip_atomic_fetch_add(rcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == BSPLIT - 1;
+    if (last) __hip_atomic_store(rcnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last || tid != 0) return;
+  const float* row = reinterpret_cast<const float*>(a.workspace) + (int64_t)r * BSPLIT * BPART;
+  auto ld = [&](int q, int i) { return __hip_atomic_load(row + q * BPART + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  float m = -INFINITY;
+  for (int q = 0; q < BSPLIT; ++q) m = fmaxf(m, ld(q, 0));
+  float ssum = 0.f;
+  for (int q = 0; q < BSPLIT; ++q) {
+    const float mq = ld(q, 0);
+    if (mq > -INFINITY) ssum += ld(q, 1) * expf(mq - m);
+  }
+  const float ls = logf(ssum);
+  int ban = 0;
+  if (st.rt) {
+    float bt_ = -INFINITY, bs_ = -INFINITY, M = -INFINITY;
+    int jt = 0x7fffffff, js = 0x7fffffff;
+    for (int q = 0; q < BSPLIT; ++q) {
+      if (better(ld(q, 2), __float_as_int(ld(q, 3)), bt_, jt)) { bt_ = ld(q, 2); jt = __float_as_int(ld(q, 3)); }
+      if (better(ld(q, 4), __float_as_int(ld(q, 5)), bs_, js)) { bs_ = ld(q, 4); js = __float_as_int(ld(q, 5)); }
+      M = fmaxf(M, ld(q, 6));
+    }
+    float S = 0.f, Sts = 0.f;
+    for (int q = 0; q < BSPLIT; ++q) {
+      if (ld(q, 6) > -INFINITY) S += ld(q, 7) * expf(ld(q, 6) - M);
+      if (ld(q, 4) > -INFINITY) Sts += ld(q, 8) * expf(ld(q, 4) - bs_);
+    }
+    if (M > -INFINITY) {
+      const float lse = logf(S);
+      const float lp_text_max = (bt_ - M) - lse;
+      const float lp_ts_max = (bs_ - M) - lse;
+      const float ts_lse = lp_ts_max > -INFINITY ? lp_ts_max + logf(Sts) : -INFINITY;
+      ban = ts_lse > lp_text_max;
+    }
+  }
+  // k best of the BSPLIT x kp candidates of the chosen list, as log-probs (lp desc, token asc)
+  const int base = 9 + (ban ? 2 * KP : 0);
+  float cv[KMAX];
+  int ci[KMAX];
+  for (int j = 0; j < K; ++j) { cv[j] = -INFINITY; ci[j] = 0x7fffffff; }
+  for (int q = 0; q < BSPLIT; ++q)
+    for (int j = 0; j < kp; ++j) {
+      const float sval = ld(q, base + 2 * j);
+      const int idx = __float_as_int(ld(q, base + 2 * j + 1));
+      if (idx == 0x7fffffff) continue;
+      const float lpv = sval > -INFINITY ? (sval - m) - ls : -INFINITY;
+      if (!better(lpv, idx, cv[K - 1], ci[K - 1])) continue;
+      float tv = lpv;
+      int ti = idx;
+      for (int i = 0; i < K; ++i)
+        if (better(tv, ti, cv[i], ci[i])) {
+          const float t1 = cv[i];
+          const int t2 = ci[i];
+          cv[i] = tv; ci[i] = ti; tv = t1; ti = t2;
+        }
+    }
+  for (int j = 0; j < K; ++j) {
+    a.cand_val[(int64_t)r * K + j] = cv[j];
+    a.cand_idx[(int64_t)r * K + j] = ci[j] == 0x7fffffff ? 0 : ci[j];
+  }
+}
+
 // K rounds of a block arg-max over n (value, key) pairs in LDS; writes the winners' positions in order.
 __device__ void block_topk(const float* val, const int* key, int n, int k, int* out_pos, float* shf, int* shi) {
   const int tid = threadIdx.x;
@@ -371,11 +606,18 @@ __global__ __launch_bounds__(BT) void beam_select_kernel(kw_beam_select_args a) 
 
 }  // namespace
 
+extern "C" size_t kw_beam_logprobs_workspace(int64_t R) {
+  return (size_t)R * BSPLIT * BPART * sizeof(float) + (size_t)R * sizeof(int);
+}
+
 extern "C" int kw_beam_logprobs(const kw_beam_logprobs_args* a, kw_stream_t stream) {
   if (!a || !a->logits || !a->suppress_mask || !a->ids || !a->cur_len || !a->cand_val || !a->cand_idx || !a->done ||
       a->R <= 0 || a->V <= 0 || a->k < 1 || a->k > KMAX || (a->n_begin_suppress > 0 && !a->begin_suppress))
     return kw_set_error_msg(KW_EINVAL, "kw_beam_logprobs: invalid arguments (k <= 16)");
-  hipLaunchKernelGGL(beam_logprobs_kernel, dim3((unsigned)a->R), dim3(ST), 0, (hipStream_t)stream, *a);
+  if (a->workspace && a->ws_bytes >= kw_beam_logprobs_workspace(a->R) && a->V <= (int64_t)BSPLIT * BT_S * BUNR)
+    hipLaunchKernelGGL(beam_logprobs_split_kernel, dim3((unsigned)a->R, BSPLIT), dim3(BT_S), 0, (hipStream_t)stream, *a);
+  else
+    hipLaunchKernelGGL(beam_logprobs_kernel, dim3((unsigned)a->R), dim3(ST), 0, (hipStream_t)stream, *a);
   KW_CHECK_LAUNCH();
   return KW_OK;
 }

@@ -71,6 +71,7 @@ class BeamLogprobsArgs(ctypes.Structure):
         ("return_timestamps", c_i32), ("ts_begin", c_i32), ("no_ts_id", c_i32), ("eos_id", c_i32),
         ("max_initial_ts", c_i32), ("ids", c_vp), ("ids_stride", c_i64), ("cur_len", c_vp),
         ("begin_index", c_i32), ("k", c_i32), ("cand_val", c_vp), ("cand_idx", c_vp), ("done", c_vp),
+        ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
     ]
 
 
@@ -111,6 +112,7 @@ EXPORTS = {
     "kw_greedy_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), c_vp]),
     "kw_greedy_step_workspace": (ctypes.c_size_t, [c_i64]),
     "kw_beam_logprobs": (ctypes.c_int, [ctypes.POINTER(BeamLogprobsArgs), c_vp]),
+    "kw_beam_logprobs_workspace": (ctypes.c_size_t, [c_i64]),
     "kw_beam_select": (ctypes.c_int, [ctypes.POINTER(BeamSelectArgs), c_vp]),
 }
 

@@ -358,6 +358,7 @@ class DecodeSession:
                 item_flags=torch.empty((B, 3), device=dev, dtype=torch.int32),
                 cand_val=torch.empty((R, 2 * nb), device=dev, dtype=torch.float32),
                 cand_idx=torch.empty((R, 2 * nb), device=dev, dtype=torch.int32),
+                lp_ws=torch.zeros(((ops.beam_logprobs_workspace_bytes(R) + 3) // 4,), device=dev, dtype=torch.float32),
             )
             sup = torch.zeros((V,), dtype=torch.uint8)
             if gen.suppress_tokens:

@@ -259,6 +259,10 @@ def cross_attn_step(q, B, q_len, H, hd, k, v, S, out, workspace):
                                       workspace.numel() * workspace.element_size(), _s()), "kw_cross_attn_step")
 
 
+def beam_logprobs_workspace_bytes(R: int) -> int:
+    return int(_lib().kw_beam_logprobs_workspace(R))
+
+
 def greedy_step_workspace_bytes(B: int) -> int:
     return int(_lib().kw_greedy_step_workspace(B))
 
@@ -322,6 +326,9 @@ class BeamStepPlan:
         a.begin_index = begin_index
         a.k = 2 * nb
         a.cand_val, a.cand_idx, a.done = st["cand_val"].data_ptr(), st["cand_idx"].data_ptr(), st["done"].data_ptr()
+        ws = st.get("lp_ws")  # split-row log-probs / top-k (kw_beam_logprobs_workspace), zero-filled once
+        a.workspace = ws.data_ptr() if ws is not None else None
+        a.ws_bytes = ws.numel() * ws.element_size() if ws is not None else 0
         b = L.BeamSelectArgs()
         b.B, b.num_beams, b.V = B, nb, V
         b.cand_val, b.cand_idx = a.cand_val, a.cand_idx

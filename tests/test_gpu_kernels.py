@@ -552,3 +552,54 @@ def test_embed_mirror():
     ref = (tok[ids[:, 5:7]].float() + pos[5:7].float()).reshape(B * q, d)
     torch.testing.assert_close(h, ref)
     assert torch.equal(hb, ref.bfloat16())
+
+
+@pytest.mark.parametrize("rt", [False, True])
+@pytest.mark.parametrize("R,V,k,n_hist", [(10, 51865, 10, 0), (10, 51865, 10, 5), (40, 51866, 6, 3), (4, 900, 16, 2)])
+def test_beam_logprobs_split_rows(rt, R, V, k, n_hist):
+    """kw_beam_logprobs split over 8 workgroups per row == the one-workgroup kernel: the same k candidate
+    tokens per row in the same order, log-probs equal up to the normaliser's summation order."""
+    import ctypes
+
+    from kwhisper import _lib as L
+    from kwhisper.config import LARGE_V3, generation_constants
+
+    gen = generation_constants(LARGE_V3)
+    P = 3
+    rng = np.random.default_rng(R * 7 + V + k + n_hist + 100 * rt)
+    eos = min(gen.eos_token_id, V - 4)
+    ts_begin = gen.timestamp_begin if V > gen.timestamp_begin else V - 3
+    hist = rng.integers(0, eos, (R, P + n_hist))
+    if n_hist:
+        hist[1, P:] = rng.integers(ts_begin, V, n_hist)
+    ids = torch.zeros((R, 64), dtype=torch.int64, device="cuda")
+    ids[:, : hist.shape[1]] = torch.from_numpy(hist)
+    cur = torch.tensor([hist.shape[1]], dtype=torch.int32, device="cuda")
+    sup = torch.zeros(V, dtype=torch.uint8, device="cuda")
+    sup[1] = 1
+    bsup = torch.tensor([0, 7], dtype=torch.int32, device="cuda")
+    done = torch.zeros(1, dtype=torch.int32, device="cuda")
+    x = (rng.standard_normal((R, V)) * 3).astype(np.float32)
+    x[::2, ts_begin:] += 3.0
+    lg = torch.from_numpy(x).cuda()
+    res = []
+    for split in (False, True):
+        cv = torch.empty((R, k), device="cuda")
+        ci = torch.empty((R, k), dtype=torch.int32, device="cuda")
+        ws = torch.zeros(ops.beam_logprobs_workspace_bytes(R) // 4 + 1, device="cuda") if split else None
+        a = L.BeamLogprobsArgs()
+        a.logits, a.R, a.V = lg.data_ptr(), R, V
+        a.suppress_mask, a.begin_suppress, a.n_begin_suppress = sup.data_ptr(), bsup.data_ptr(), 2
+        a.return_timestamps, a.ts_begin, a.no_ts_id, a.eos_id = int(rt), ts_begin, ts_begin - 1, eos
+        a.max_initial_ts = 50
+        a.ids, a.ids_stride, a.cur_len, a.begin_index, a.k = ids.data_ptr(), 64, cur.data_ptr(), P, k
+        a.cand_val, a.cand_idx, a.done = cv.data_ptr(), ci.data_ptr(), done.data_ptr()
+        a.workspace = ws.data_ptr() if ws is not None else None
+        a.ws_bytes = ws.numel() * 4 if ws is not None else 0
+        for _ in range(2):
+            L.check(L.load().kw_beam_logprobs(ctypes.byref(a), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)),
+                    "kw_beam_logprobs")
+        torch.cuda.synchronize()
+        res.append((cv.cpu().numpy(), ci.cpu().numpy()))
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-6, atol=1e-5)
