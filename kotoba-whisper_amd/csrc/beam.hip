@@ -267,9 +267,19 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
     sa = bl_sum(sa, shf);
     sts = bl_sum(sts, shf);
   }
-  // the slice's KP best processed scores (all tokens; and timestamps only, for the text-ban case)
+  // the slice's KP best processed scores (all tokens; and timestamps only, for the text-ban case):
+  // each wave takes its own kp best by shuffle-only rounds (no workgroup barrier per round), then wave 0
+  // takes the slice's kp best of the waves' 8 x kp
   const int kp = min(K + 4, KP);
-  for (int list = 0; list < (st.rt ? 2 : 1); ++list) {
+  const int lane = tid & 63, wv = tid >> 6;
+  __shared__ float wcv[2][BT_S / 64][KP];
+  __shared__ int wci[2][BT_S / 64][KP];
+#ifdef KW_BEAM_LAB_SKIP_TOPK
+  const int nlist = 0;  // lab: time the kernel without the slice top-k
+#else
+  const int nlist = st.rt ? 2 : 1;
+#endif
+  for (int list = 0; list < nlist; ++list) {
     unsigned taken = 0;
     for (int j = 0; j < kp; ++j) {
       float bv = -INFINITY;
@@ -281,12 +291,52 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
           bv = sv[u]; bi = v; bu = u;
         }
       }
-      int bt = tid;
-      bl_argmax(bv, bi, bt, shf, shi);
-      if (tid == bt && bu >= 0 && bi == v0 + tid + bu * BT_S) taken |= 1u << bu;
-      if (tid == 0) {
-        pub[9 + list * 2 * KP + 2 * j] = bv;
-        pub[9 + list * 2 * KP + 2 * j + 1] = __int_as_float(bi);
+      float gv = bv;
+      int gi = bi, gl = lane;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float ov = __shfl_xor(gv, o, 64);
+        const int oi = __shfl_xor(gi, o, 64), ol = __shfl_xor(gl, o, 64);
+        if (better(ov, oi, gv, gi)) { gv = ov; gi = oi; gl = ol; }
+      }
+      if (lane == gl && bu >= 0 && gi == bi) taken |= 1u << bu;
+      if (lane == 0) { wcv[list][wv][j] = gv; wci[list][wv][j] = gi; }
+    }
+  }
+  __syncthreads();
+  if (wv == 0) {
+    for (int list = 0; list < nlist; ++list) {
+      // lane l holds candidates l and l + 64 of the waves' 8 x kp (kp <= 20: 160 <= 128 + 32 ... two slots)
+      float c0 = -INFINITY, c1 = -INFINITY;
+      int i0 = 0x7fffffff, i1 = 0x7fffffff;
+      const int n = (BT_S / 64) * kp;
+      if (lane < n) { c0 = wcv[list][lane / kp][lane % kp]; i0 = wci[list][lane / kp][lane % kp]; }
+      if (lane + 64 < n) { c1 = wcv[list][(lane + 64) / kp][(lane + 64) % kp]; i1 = wci[list][(lane + 64) / kp][(lane + 64) % kp]; }
+      float c2 = -INFINITY;
+      int i2 = 0x7fffffff;
+      if (lane + 128 < n) { c2 = wcv[list][(lane + 128) / kp][(lane + 128) % kp]; i2 = wci[list][(lane + 128) / kp][(lane + 128) % kp]; }
+      for (int j = 0; j < kp; ++j) {
+        float bv = c0;
+        int bi = i0, bs = 0;
+        if (better(c1, i1, bv, bi)) { bv = c1; bi = i1; bs = 1; }
+        if (better(c2, i2, bv, bi)) { bv = c2; bi = i2; bs = 2; }
+        float gv = bv;
+        int gi = bi, gl = lane;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+          const float ov = __shfl_xor(gv, o, 64);
+          const int oi = __shfl_xor(gi, o, 64), ol = __shfl_xor(gl, o, 64);
+          if (better(ov, oi, gv, gi)) { gv = ov; gi = oi; gl = ol; }
+        }
+        if (lane == gl) {
+          if (bs == 0) { c0 = -INFINITY; i0 = 0x7fffffff; }
+          else if (bs == 1) { c1 = -INFINITY; i1 = 0x7fffffff; }
+          else { c2 = -INFINITY; i2 = 0x7fffffff; }
+        }
+        if (lane == 0) {
+          pub[9 + list * 2 * KP + 2 * j] = gv;
+          pub[9 + list * 2 * KP + 2 * j + 1] = __int_as_float(gi);
+        }
       }
     }
   }
@@ -308,9 +358,17 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
     if (last) __hip_atomic_store(rcnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
-  if (!last || tid != 0) return;
+  if (!last) return;
+  // the row's partials into LDS by the whole workgroup (one round trip), then one thread merges
+  __shared__ float allp[BSPLIT * BPART];
   const float* row = reinterpret_cast<const float*>(a.workspace) + (int64_t)r * BSPLIT * BPART;
-  auto ld = [&](int q, int i) { return __hip_atomic_load(row + q * BPART + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  for (int i = tid; i < BSPLIT * BPART; i += BT_S)
+    allp[i] = (i % BPART) < npub ? __hip_atomic_load(row + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+  __syncthreads();
+  if (wv != 0) return;
+  // wave 0 merges: every lane derives the row's normaliser and the text-ban decision from the BSPLIT
+  // slice records (identical on all lanes), then k rounds of a wave arg-max pick the candidates
+  auto ld = [&](int q, int i) { return allp[q * BPART + i]; };
   float m = -INFINITY;
   for (int q = 0; q < BSPLIT; ++q) m = fmaxf(m, ld(q, 0));
   float ssum = 0.f;
@@ -341,30 +399,48 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
       ban = ts_lse > lp_text_max;
     }
   }
-  // k best of the BSPLIT x kp candidates of the chosen list, as log-probs (lp desc, token asc)
+  // candidates of the chosen list as log-probs, three per lane (BSPLIT x kp <= 192)
   const int base = 9 + (ban ? 2 * KP : 0);
-  float cv[KMAX];
-  int ci[KMAX];
-  for (int j = 0; j < K; ++j) { cv[j] = -INFINITY; ci[j] = 0x7fffffff; }
-  for (int q = 0; q < BSPLIT; ++q)
-    for (int j = 0; j < kp; ++j) {
+  const int n = BSPLIT * kp;
+  float c[3];
+  int ci3[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int e = lane + 64 * t;
+    c[t] = -INFINITY;
+    ci3[t] = 0x7fffffff;
+    if (e < n) {
+      const int q = e / kp, j = e - q * kp;
       const float sval = ld(q, base + 2 * j);
       const int idx = __float_as_int(ld(q, base + 2 * j + 1));
-      if (idx == 0x7fffffff) continue;
-      const float lpv = sval > -INFINITY ? (sval - m) - ls : -INFINITY;
-      if (!better(lpv, idx, cv[K - 1], ci[K - 1])) continue;
-      float tv = lpv;
-      int ti = idx;
-      for (int i = 0; i < K; ++i)
-        if (better(tv, ti, cv[i], ci[i])) {
-          const float t1 = cv[i];
-          const int t2 = ci[i];
-          cv[i] = tv; ci[i] = ti; tv = t1; ti = t2;
-        }
+      if (idx != 0x7fffffff) {
+        c[t] = sval > -INFINITY ? (sval - m) - ls : -INFINITY;
+        ci3[t] = idx;
+      }
     }
+  }
   for (int j = 0; j < K; ++j) {
-    a.cand_val[(int64_t)r * K + j] = cv[j];
-    a.cand_idx[(int64_t)r * K + j] = ci[j] == 0x7fffffff ? 0 : ci[j];
+    float bv = c[0];
+    int bi = ci3[0], bs = 0;
+    if (better(c[1], ci3[1], bv, bi)) { bv = c[1]; bi = ci3[1]; bs = 1; }
+    if (better(c[2], ci3[2], bv, bi)) { bv = c[2]; bi = ci3[2]; bs = 2; }
+    float gv = bv;
+    int gi = bi, gl = lane;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(gv, o, 64);
+      const int oi = __shfl_xor(gi, o, 64), ol = __shfl_xor(gl, o, 64);
+      if (better(ov, oi, gv, gi)) { gv = ov; gi = oi; gl = ol; }
+    }
+    if (lane == gl && gi == bi && bi != 0x7fffffff) {
+      if (bs == 0) { c[0] = -INFINITY; ci3[0] = 0x7fffffff; }
+      else if (bs == 1) { c[1] = -INFINITY; ci3[1] = 0x7fffffff; }
+      else { c[2] = -INFINITY; ci3[2] = 0x7fffffff; }
+    }
+    if (lane == 0) {
+      a.cand_val[(int64_t)r * K + j] = gv;
+      a.cand_idx[(int64_t)r * K + j] = gi == 0x7fffffff ? 0 : gi;
+    }
   }
 }
 

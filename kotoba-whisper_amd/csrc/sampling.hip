@@ -163,14 +163,18 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_kernel(kw_sampler_a
   if (prev != NSPLIT - 1) return;
   __hip_atomic_store(rcnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const float* row = reinterpret_cast<const float*>(a.workspace) + (int64_t)b * NSPLIT * PART;
+  float pv[NSPLIT];
+  int pi[NSPLIT];
+#pragma unroll
+  for (int q = 0; q < NSPLIT; ++q) {  // every partial load in flight before the first compare
+    pv[q] = __hip_atomic_load(row + PART * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    pi[q] = __hip_atomic_load(reinterpret_cast<const int*>(row) + PART * q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   float bb = -INFINITY;
   int ii = 0x7fffffff;
-  for (int q = 0; q < NSPLIT; ++q) {  // slice order = index order: strict > keeps the first max
-    const float pv = __hip_atomic_load(row + PART * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int pi = __hip_atomic_load(reinterpret_cast<const int*>(row) + PART * q + 1, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-    if (pv > bb || (pv == bb && pi < ii)) { bb = pv; ii = pi; }
-  }
+#pragma unroll
+  for (int q = 0; q < NSPLIT; ++q)  // slice order = index order: strict > keeps the first max
+    if (pv[q] > bb || (pv[q] == bb && pi[q] < ii)) { bb = pv[q]; ii = pi[q]; }
   if (ii == 0x7fffffff) ii = 0;
   const int64_t tok = fin ? (int64_t)a.pad_id : (int64_t)ii;
   a.ids[(int64_t)b * a.ids_stride + L] = tok;
@@ -338,7 +342,9 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_ts_kernel(kw_sample
   __hip_atomic_store(rcnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const float* row = reinterpret_cast<const float*>(a.workspace) + (int64_t)b * NSPLIT * PART;
   float P[NSPLIT][7];
-  for (int q = 0; q < NSPLIT; ++q)
+#pragma unroll
+  for (int q = 0; q < NSPLIT; ++q)  // every partial load in flight before the merge
+#pragma unroll
     for (int i = 0; i < 7; ++i) P[q][i] = __hip_atomic_load(row + PART * q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   float bt = -INFINITY, bs = -INFINITY, M = -INFINITY, Mts = -INFINITY;
   int jt = 0x7fffffff, js = 0x7fffffff;
