@@ -62,3 +62,29 @@ def beam_gen_dict(shape, eos=None) -> dict:
     if eos is not None:
         d["eos_token_id"] = eos
     return d
+
+
+def long_audio(kind, seed, seconds):
+    """tools/make_fixtures.py long_audio: > 30 s clips, the seeded 30 s clips of ``kind`` concatenated."""
+    n = int(seconds * 16000)
+    parts, k = [], 0
+    while sum(len(p) for p in parts) < n:
+        parts.append(getattr(S, f"{kind}_audio")(seed + 10 * k))
+        k += 1
+    return np.concatenate(parts)[:n].astype(np.float32)
+
+
+def longform_inputs(clips, n_mels=80):
+    """Batched long-form inputs as the fixture made them: transformers' WhisperFeatureExtractor with
+    truncation=False, padding="longest" and the frame-level attention mask (generation_whisper.py:588-589)."""
+    from transformers import WhisperFeatureExtractor
+
+    fe = WhisperFeatureExtractor(feature_size=n_mels)
+    audio = []
+    for c in clips:
+        kind, seed, sec = str(c).split(":")
+        audio.append(long_audio(kind, int(seed), float(sec)))
+    inp = fe(audio, sampling_rate=16000, return_tensors="np", truncation=False, padding="longest",
+             return_attention_mask=True)
+    one = fe([audio[1]], sampling_rate=16000, return_tensors="np", truncation=False, padding="longest")
+    return inp["input_features"], inp["attention_mask"], one["input_features"]

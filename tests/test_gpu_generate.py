@@ -256,3 +256,26 @@ def test_generate_pipelined_matches_per_batch(gold, tiny32, ts):
     for a, b in zip(got2, want[:2]):
         np.testing.assert_array_equal(a.cpu().numpy(), b.numpy())
     assert list(tiny32.generate_pipelined([], **kw)) == []
+
+
+def test_tiny_fp32_longform_bitexact(gold, tiny32):
+    """Long-form generate (> 3000 mel frames: the seek loop re-encodes shifted 30 s windows,
+    generation_whisper.py:785-903) == transformers on the same features: batched with an attention mask
+    (tokens and segments), and one clip without a mask."""
+    from _util import longform_inputs, segments_of
+
+    g = gold("tiny_longform_fp32")
+    feats, mask, one = longform_inputs(g["clips"])
+    res = tiny32.generate(torch.from_numpy(feats).cuda(), attention_mask=torch.from_numpy(mask).cuda(),
+                          language="ja", task="transcribe", return_timestamps=True, return_segments=True)
+    np.testing.assert_array_equal(res["sequences"].cpu().numpy(), g["long_ts_segments_tokens"])
+    want = segments_of(g["long_ts_segments_segments"])
+    got = [[(s["start"], s["end"], len(s["tokens"])) for s in row] for row in res["segments"]]
+    assert [[x[2] for x in r] for r in got] == [[x[2] for x in r] for r in want]
+    for rg, rw in zip(got, want):
+        np.testing.assert_allclose([x[:2] for x in rg], [x[:2] for x in rw], atol=1e-9)
+    plain = tiny32.generate(torch.from_numpy(feats).cuda(), attention_mask=torch.from_numpy(mask).cuda(),
+                            language="ja", task="transcribe", return_timestamps=True)
+    np.testing.assert_array_equal(plain.cpu().numpy(), g["long_ts_tokens"])
+    single = tiny32.generate(torch.from_numpy(one).cuda(), language="ja", task="transcribe", return_timestamps=True)
+    np.testing.assert_array_equal(single.cpu().numpy(), g["long_single_tokens"])

@@ -121,3 +121,21 @@ def test_oracle_large_generate(gold, shape, tag):
     toks = og.generate(model, feats, gen_dict(shape), max_length=int(g["max_length"]), language="ja",
                        task="transcribe", return_timestamps=False)
     np.testing.assert_array_equal(toks, g["greedy_tokens"])
+
+
+def test_oracle_tiny_longform(gold, tiny):
+    """Long-form (> 3000 frames) seek loop: batched with an attention mask, and one clip without."""
+    from _util import longform_inputs
+
+    g = gold("tiny_longform_fp32")
+    feats, mask, one = longform_inputs(g["clips"])
+    res = og.generate(tiny, feats, gen_dict(TINY), language="ja", task="transcribe", return_timestamps=True,
+                      attention_mask=mask, return_segments=True)
+    np.testing.assert_array_equal(res["sequences"], g["long_ts_segments_tokens"])
+    want = segments_of(g["long_ts_segments_segments"])
+    got = [[(s["start"], s["end"], len(s["tokens"])) for s in row] for row in res["segments"]]
+    assert [[x[2] for x in r] for r in got] == [[x[2] for x in r] for r in want]
+    for rg, rw in zip(got, want):
+        np.testing.assert_allclose([x[:2] for x in rg], [x[:2] for x in rw], atol=1e-9)
+    np.testing.assert_array_equal(og.generate(tiny, one, gen_dict(TINY), language="ja", task="transcribe",
+                                              return_timestamps=True), g["long_single_tokens"])

@@ -174,6 +174,49 @@ def beam_fixtures():
     np.savez_compressed(os.path.join(GOLD, "tiny_beam_fp32.npz"), **out)
 
 
+LONG_CLIPS = [("tone", 0, 45.0), ("dummy", 3, 70.0), ("dummy", 4, 12.0)]
+
+
+def long_audio(kind, seed, seconds):
+    """> 30 s clips for the long-form seek loop: the seeded 30 s clips of ``kind`` concatenated."""
+    n = int(seconds * 16000)
+    parts, k = [], 0
+    while sum(len(p) for p in parts) < n:
+        parts.append(clip_audio(kind, seed + 10 * k))
+        k += 1
+    return np.concatenate(parts)[:n].astype(np.float32)
+
+
+def longform_fixtures():
+    """tests/golden/tiny_longform_fp32.npz: long-form (> 3000 frames) generate through the real HF seek loop
+    (generation_whisper.py:785-903): batched with an attention mask, and a single clip without one."""
+    t0 = time.time()
+    m = hf_model(TINY)
+    fe = WhisperFeatureExtractor(feature_size=TINY.num_mel_bins)
+    audio = [long_audio(k, s, sec) for k, s, sec in LONG_CLIPS]
+    inp = fe(audio, sampling_rate=16000, return_tensors="pt", truncation=False, padding="longest",
+             return_attention_mask=True)
+    out = {"clips": np.array([f"{k}:{s}:{sec}" for k, s, sec in LONG_CLIPS])}
+    for name, kw in [("long_ts", dict(language="ja", task="transcribe")),
+                     ("long_ts_segments", dict(language="ja", task="transcribe", return_segments=True))]:
+        m.generation_config, _ = hf_gen_config(TINY)
+        res = run_generate(m, inp["input_features"], attention_mask=inp["attention_mask"], return_timestamps=True,
+                           **kw)
+        if isinstance(res, torch.Tensor):
+            out[f"{name}_tokens"] = res.numpy().astype(np.int64)
+        else:
+            out[f"{name}_tokens"] = res["sequences"].numpy().astype(np.int64)
+            segs = [[(float(x["start"]), float(x["end"]), len(x["tokens"])) for x in row] for row in res["segments"]]
+            out[f"{name}_segments"] = np.array(json.dumps(segs))
+        print(f"  tiny_longform:{name} {tuple(out[f'{name}_tokens'].shape)} ({time.time() - t0:.1f}s)")
+    one = fe([audio[1]], sampling_rate=16000, return_tensors="pt", truncation=False, padding="longest")
+    m.generation_config, _ = hf_gen_config(TINY)
+    res = run_generate(m, one["input_features"], return_timestamps=True, language="ja", task="transcribe")
+    out["long_single_tokens"] = res.numpy().astype(np.int64)
+    np.savez_compressed(os.path.join(GOLD, "tiny_longform_fp32.npz"), **out)
+    print(f"tiny_longform fixtures done in {time.time() - t0:.1f}s")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
@@ -198,6 +241,8 @@ def main():
     ]
     if a.only in (None, "beam"):
         beam_fixtures()
+    if a.only in (None, "longform"):
+        longform_fixtures()
     if a.only in (None, "tiny"):
         cases = [("dummy", 0), ("dummy", 1), ("tone", 0), ("tone", 1)]
         model_fixtures(TINY, "tiny_fp32", cases, 128, tiny_modes)
