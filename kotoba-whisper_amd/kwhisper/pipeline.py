@@ -293,11 +293,35 @@ class ASRPipeline:
             out = [dict(audio=inputs[a:b], is_last=last, stride=st, **extra)
                    for a, b, last, st in chunk_iter(inputs.shape[0], chunk_len, sl, sr_)]
         else:
-            if inputs.shape[0] > self.feature_extractor.n_samples:
-                raise NotImplementedError("un-chunked inputs longer than 30 s (long-form pipeline) are not supported; "
-                                          "pass chunk_length_s")
+            # one item; longer than 30 s -> Whisper long-form (seek loop in generate, :449-458)
             out = [dict(audio=inputs, is_last=True, **extra)]
         return out
+
+    def _batch_features(self, audios):
+        """Each item through the feature extractor as the reference's preprocess does (<= 30 s: padded to
+        30 s; longer: truncation=False, padding="longest", :449-470), then the batch collated as its
+        pad_collate_fn does: features right-padded with the extractor's padding value to the longest item,
+        attention masks with zeros."""
+        fe = self.feature_extractor
+        if all(len(x) <= fe.n_samples for x in audios):
+            f = fe(audios, sampling_rate=fe.sampling_rate, return_attention_mask=True)
+            return f["input_features"], f["attention_mask"]
+        items = []
+        for x in audios:
+            if len(x) > fe.n_samples:
+                items.append(fe([x], sampling_rate=fe.sampling_rate, truncation=False, padding="longest",
+                                return_attention_mask=True))
+            else:
+                items.append(fe([x], sampling_rate=fe.sampling_rate, return_attention_mask=True))
+        T = max(f["input_features"].shape[-1] for f in items)
+        n_mels = items[0]["input_features"].shape[1]
+        feats = torch.full((len(items), n_mels, T), float(fe.padding_value), device=fe.device)
+        mask = torch.zeros((len(items), T), dtype=torch.int32, device=fe.device)
+        for i, f in enumerate(items):
+            t = f["input_features"].shape[-1]
+            feats[i, :, :t] = f["input_features"][0]
+            mask[i, : f["attention_mask"].shape[-1]] = f["attention_mask"][0]
+        return feats, mask
 
     # ---- forward (:483-560) + postprocess (:600-710) -----------------------------------------------------
     def __call__(self, inputs, *, chunk_length_s=None, stride_length_s=None, return_timestamps=None,
@@ -327,8 +351,8 @@ class ASRPipeline:
         tokens = [None] * len(flat)
         for b0 in range(0, len(flat), bs):
             batch = flat[b0: b0 + bs]
-            feats = fe([c["audio"] for _, c in batch], sampling_rate=fe.sampling_rate, return_attention_mask=True)
-            out = self.model.generate(feats["input_features"], attention_mask=feats["attention_mask"], **gk)
+            feats, mask = self._batch_features([c["audio"] for _, c in batch])
+            out = self.model.generate(feats, attention_mask=mask, **gk)
             ids = out["sequences"] if isinstance(out, dict) else out
             ids = ids.cpu()
             for j in range(len(batch)):

@@ -279,3 +279,44 @@ def test_tiny_fp32_longform_bitexact(gold, tiny32):
     np.testing.assert_array_equal(plain.cpu().numpy(), g["long_ts_tokens"])
     single = tiny32.generate(torch.from_numpy(one).cuda(), language="ja", task="transcribe", return_timestamps=True)
     np.testing.assert_array_equal(single.cpu().numpy(), g["long_single_tokens"])
+
+
+def test_asr_pipeline_unchunked_longform(gold, tiny32):
+    """ASRPipeline without chunk_length_s on > 30 s clips: each item is one long-form generate (the seek
+    loop), batched with the reference's collate (features padded, attention masks); == transformers'
+    _decode_asr over the HF long-form token rows of the same clips (fixture tiny_longform_fp32).
+    The feature extractor is transformers' own here, so the comparison is exact (ours is tested apart)."""
+    from transformers import WhisperFeatureExtractor as HFFE
+    from transformers.models.whisper.tokenization_whisper import _decode_asr
+
+    from _util import long_audio
+    from kwhisper.pipeline import ASRPipeline
+    from test_pipeline import StubTokenizer
+
+    class _FE:
+        sampling_rate, n_samples, padding_value, chunk_length = 16000, 480000, 0.0, 30
+        device = torch.device("cuda")
+
+        def __init__(self):
+            self.fe = HFFE(feature_size=TINY.num_mel_bins)
+
+        def __call__(self, audio, **kw):
+            kw.pop("device", None)
+            out = self.fe(audio, return_tensors="pt", **kw)
+            return {k: v.cuda() for k, v in out.items()}
+
+    g = gold("tiny_longform_fp32")
+    clips = []
+    for c in g["clips"]:
+        kind, seed, sec = str(c).split(":")
+        clips.append(long_audio(kind, int(seed), float(sec)))
+    tk = StubTokenizer()
+    tk.all_special_ids = tk.all_special_ids + [tiny32.generation_config.pad_token_id]
+    pipe = ASRPipeline(tiny32, feature_extractor=_FE(), tokenizer=tk, batch_size=3,
+                       generate_kwargs=dict(language="ja", task="transcribe"))
+    got = pipe([{"array": c, "sampling_rate": 16000} for c in clips], return_timestamps=True)
+    for i, res in enumerate(got):
+        text, optional = _decode_asr(tk, [{"tokens": torch.from_numpy(g["long_ts_tokens"][i: i + 1])}],
+                                     return_timestamps=True, return_language=None, time_precision=0.02)
+        assert res["text"] == text and len(text) > 0
+        assert res["chunks"] == optional["chunks"]
