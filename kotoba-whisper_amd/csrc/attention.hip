@@ -606,9 +606,9 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
                                                                const T* __restrict__ kc, const T* __restrict__ vc,
                                                                int S, int chunk, float* __restrict__ ws,
                                                                int* __restrict__ cnt, T* __restrict__ out) {
-  static_assert(QN * HD <= 256, "one combine thread per (row, dim)");
-  __shared__ float red[QN][4][64];
-  __shared__ float stat[QN][8];
+  static_assert(QN % 4 == 0 && QN <= 8, "rows in blocks of 4, at most 8 (the beam limit)");
+  __shared__ float red[4][4][64];
+  __shared__ float stat[4][8];
   __shared__ int last;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ngrp = (q_len + QN - 1) / QN;
@@ -626,117 +626,141 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
   for (int j = 0; j < 8; ++j) kr[j] = ld_row8<T>(kb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8);
 #pragma unroll
   for (int j = 0; j < 8; ++j) vr[j] = ld_row8<T>(vb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8);
-  float sc[QN][8];
+  // rows in blocks of 4 (one combine thread per (row, dim) per block): the K/V registers stay live
+  // across the blocks, so an item's QN rows cost ONE K/V pass
+  float mrow[QN], lrow[QN], orow_acc[QN];
 #pragma unroll
-  for (int r = 0; r < QN; ++r) {
-    float qv[8];
-    load8<T>(q + ((int64_t)(b * q_len + qi0 + min(r, nq - 1))) * H * HD + h * HD + sub * 8, qv);
-    float mx = -INFINITY;
+  for (int r0 = 0; r0 < QN; r0 += 4) {
+    if (r0 >= nq) break;
+    float sc[4][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      float kv[8];
-      unpack8<T>(kr[j], kv);
-      float sj = 0.f;
+    for (int r = 0; r < 4; ++r) {
+      float qv[8];
+      load8<T>(q + ((int64_t)(b * q_len + qi0 + min(r0 + r, nq - 1))) * H * HD + h * HD + sub * 8, qv);
+      float mx = -INFINITY;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kv[i], sj);
-      sj += __shfl_xor(sj, 1, 64);
-      sj += __shfl_xor(sj, 2, 64);
-      sj += __shfl_xor(sj, 4, 64);
-      sc[r][j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
-      mx = fmaxf(mx, sc[r][j]);
+      for (int j = 0; j < 8; ++j) {
+        float kv[8];
+        unpack8<T>(kr[j], kv);
+        float sj = 0.f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kv[i], sj);
+        sj += __shfl_xor(sj, 1, 64);
+        sj += __shfl_xor(sj, 2, 64);
+        sj += __shfl_xor(sj, 4, 64);
+        sc[r][j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
+        mx = fmaxf(mx, sc[r][j]);
+      }
+      mx = wave_max(mx);
+      if (lane == 0) stat[r][wave] = mx;
     }
-    mx = wave_max(mx);
-    if (lane == 0) stat[r][wave] = mx;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float m = fmaxf(fmaxf(stat[r][0], stat[r][1]), fmaxf(stat[r][2], stat[r][3]));
+      mrow[r0 + r] = m;
+      float lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[r][j] - m) : 0.f;
+        lsum += pj;
+        float vv[8];
+        unpack8<T>(vr[j], vv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        acc[i] += __shfl_xor(acc[i], 8, 64);
+        acc[i] += __shfl_xor(acc[i], 16, 64);
+        acc[i] += __shfl_xor(acc[i], 32, 64);
+      }
+      lsum = wave_sum(lsum) * 0.125f;
+      if (lane < 8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) red[r][wave][lane * 8 + i] = acc[i];
+      }
+      if (lane == 0) stat[r][4 + wave] = lsum;
+    }
+    __syncthreads();
+    // thread (row rr = tid / 64 of this block, dim dd) collects its element
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (r == (tid >> 6)) {
+        lrow[r0 / 4] = (stat[r][4] + stat[r][5]) + (stat[r][6] + stat[r][7]);
+        orow_acc[r0 / 4] = (red[r][0][lane] + red[r][1][lane]) + (red[r][2][lane] + red[r][3][lane]);
+      }
+    __syncthreads();  // stat / red are rewritten by the next block
   }
-  __syncthreads();
-  float mrow[QN];
+  constexpr int NB = QN / 4;
+  const int dd = lane;
+  bool last_any = false;
+  if (ns > 1) {
+    // publish every owned (row, dim) partial, then one arrival per row group
 #pragma unroll
-  for (int r = 0; r < QN; ++r) {
-    const float m = fmaxf(fmaxf(stat[r][0], stat[r][1]), fmaxf(stat[r][2], stat[r][3]));
-    mrow[r] = m;
-    float lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int bk = 0; bk < NB; ++bk) {
+      const int rr = bk * 4 + (tid >> 6);
+      if (rr < nq) {
+        const int row = (b * q_len + qi0 + rr) * H + h;
+        float* w = ws + (int64_t)row * ns * (HD + 2) + (int64_t)split * (HD + 2);
+        __hip_atomic_store(w + 2 + dd, orow_acc[bk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dd == 0) {
+          float mm = 0.f;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[r][j] - m) : 0.f;
-      lsum += pj;
-      float vv[8];
-      unpack8<T>(vr[j], vv);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
+          for (int r = 0; r < QN; ++r)
+            if (r == rr) mm = mrow[r];
+          __hip_atomic_store(w, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(w + 1, lrow[bk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
     }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      acc[i] += __shfl_xor(acc[i], 8, 64);
-      acc[i] += __shfl_xor(acc[i], 16, 64);
-      acc[i] += __shfl_xor(acc[i], 32, 64);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* c = cnt + (b * q_len + qi0) * H + h;  // one counter per row group
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = prev == ns - 1;
+      if (prev == ns - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    lsum = wave_sum(lsum) * 0.125f;
-    if (lane < 8) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) red[r][wave][lane * 8 + i] = acc[i];
-    }
-    if (lane == 0) stat[r][4 + wave] = lsum;
+    __syncthreads();
+    last_any = last;
+    if (!last_any) return;
   }
-  __syncthreads();
-  // thread (row rr, dim dd) owns one output element from here on
-  const int rr = tid >> 6, dd = tid & 63;
-  const bool mine = rr < nq;
-  float m = 0.f, l = 0.f, o = 0.f;
 #pragma unroll
-  for (int r = 0; r < QN; ++r)
-    if (r == rr) {
-      m = mrow[r];
-      l = (stat[r][4] + stat[r][5]) + (stat[r][6] + stat[r][7]);
-      o = (red[r][0][dd] + red[r][1][dd]) + (red[r][2][dd] + red[r][3][dd]);
+  for (int bk = 0; bk < NB; ++bk) {
+    const int rr = bk * 4 + (tid >> 6);
+    if (rr >= nq) continue;
+    T* orow = out + (int64_t)(b * q_len + qi0 + rr) * H * HD + h * HD;
+    if (ns == 1) {
+      TypeIO<T>::st(orow + dd, orow_acc[bk] / lrow[bk]);
+      continue;
     }
-  const int row = (b * q_len + qi0 + min(rr, nq - 1)) * H + h;
-  T* orow = out + (int64_t)(b * q_len + qi0 + min(rr, nq - 1)) * H * HD + h * HD;
-  if (ns == 1) {
-    if (mine) TypeIO<T>::st(orow + dd, o / l);
-    return;
-  }
-  float* part = ws + (int64_t)row * ns * (HD + 2);
-  if (mine) {
-    float* w = part + (int64_t)split * (HD + 2);
-    __hip_atomic_store(w + 2 + dd, o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (dd == 0) {
-      __hip_atomic_store(w, m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(w + 1, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* c = cnt + (b * q_len + qi0) * H + h;  // one counter per row group
-  if (tid == 0) {
-    const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last = prev == ns - 1;
-    if (prev == ns - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!last || !mine) return;
-  constexpr int NSMAX = 8;
-  float ms[NSMAX], ls[NSMAX], os[NSMAX];
+    const int row = (b * q_len + qi0 + rr) * H + h;
+    const float* part = ws + (int64_t)row * ns * (HD + 2);
+    constexpr int NSMAX = 8;
+    float ms[NSMAX], ls[NSMAX], os[NSMAX];
 #pragma unroll
-  for (int qq = 0; qq < NSMAX; ++qq) {
-    if (qq < ns) {
-      ms[qq] = __hip_atomic_load(part + qq * (HD + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      ls[qq] = __hip_atomic_load(part + qq * (HD + 2) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      os[qq] = __hip_atomic_load(part + qq * (HD + 2) + 2 + dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int qq = 0; qq < NSMAX; ++qq) {
+      if (qq < ns) {
+        ms[qq] = __hip_atomic_load(part + qq * (HD + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ls[qq] = __hip_atomic_load(part + qq * (HD + 2) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        os[qq] = __hip_atomic_load(part + qq * (HD + 2) + 2 + dd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
+    float M = -INFINITY;
+#pragma unroll
+    for (int qq = 0; qq < NSMAX; ++qq)
+      if (qq < ns) M = fmaxf(M, ms[qq]);
+    float lt = 0.f, ot = 0.f;
+#pragma unroll
+    for (int qq = 0; qq < NSMAX; ++qq)
+      if (qq < ns) {
+        const float f = expf(ms[qq] - M);
+        lt = fmaf(ls[qq], f, lt);
+        ot = fmaf(os[qq], f, ot);
+      }
+    TypeIO<T>::st(orow + dd, ot / lt);
   }
-  float M = -INFINITY;
-#pragma unroll
-  for (int qq = 0; qq < NSMAX; ++qq)
-    if (qq < ns) M = fmaxf(M, ms[qq]);
-  float lt = 0.f, ot = 0.f;
-#pragma unroll
-  for (int qq = 0; qq < NSMAX; ++qq)
-    if (qq < ns) {
-      const float f = expf(ms[qq] - M);
-      lt = fmaf(ls[qq], f, lt);
-      ot = fmaf(os[qq], f, ot);
-    }
-  TypeIO<T>::st(orow + dd, ot / lt);
 }
 
 // decoder self-attention for one new position (q_len == 1): split 0 appends k/v at L-1; each split
@@ -875,9 +899,13 @@ extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q
   dim3 grid((unsigned)(B * q_len * H), (unsigned)ns);
   float* part = (float*)workspace;
   int* cnt = (int*)((char*)workspace + cross_partials_bytes(B, q_len, H, S));
-  if (dtype == KW_DT_BF16 && q_len > 1) {  // several rows per item (prefill, beams): one K/V pass per 4 rows
-    const dim3 gm((unsigned)(B * ((q_len + 3) / 4) * H), (unsigned)ns);
+  if (dtype == KW_DT_BF16 && q_len > 1 && q_len <= 4) {  // several rows per item (prefill, beams): one K/V pass
+    const dim3 gm((unsigned)(B * H), (unsigned)ns);
     hipLaunchKernelGGL((cross_attn_multi_kernel<bf16_t, 4>), gm, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
+                       (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
+  } else if (dtype == KW_DT_BF16 && q_len > 4) {  // up to 8 rows per K/V pass (beam 5-8), groups of 8 beyond
+    const dim3 gm((unsigned)(B * ((q_len + 7) / 8) * H), (unsigned)ns);
+    hipLaunchKernelGGL((cross_attn_multi_kernel<bf16_t, 8>), gm, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
   } else if (dtype == KW_DT_BF16)
     hipLaunchKernelGGL(cross_attn_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,

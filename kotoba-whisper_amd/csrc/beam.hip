@@ -29,6 +29,36 @@ constexpr float NEG = -1.0e9f;
 
 __device__ __forceinline__ bool better(float a, int ia, float b, int ib) { return a > b || (a == b && ia < ib); }
 
+// (score, token) as one 64-bit key ordered like better(): monotonic float bits above, ~token below.
+// -0 is folded into +0 first (better() compares values).  Key 0 = no candidate.
+__device__ __forceinline__ uint64_t bkey(float s, int v) {
+  uint32_t b = __float_as_uint(s + 0.0f);
+  b = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+  return ((uint64_t)b << 32) | (uint32_t)(0xFFFFFFFFu - (uint32_t)v);
+}
+__device__ __forceinline__ float bkey_val(uint64_t k) {
+  const uint32_t b = (uint32_t)(k >> 32);
+  return __uint_as_float((b & 0x80000000u) ? (b & 0x7fffffffu) : ~b);
+}
+__device__ __forceinline__ int bkey_idx(uint64_t k) { return (int)(0xFFFFFFFFu - (uint32_t)k); }
+// insert k into the descending triple (c0, c1, c2)
+__device__ __forceinline__ void bins3(uint64_t k, uint64_t& c0, uint64_t& c1, uint64_t& c2) {
+  const uint64_t h0 = k > c0 ? k : c0, l0 = k > c0 ? c0 : k;
+  const uint64_t h1 = l0 > c1 ? l0 : c1, l1 = l0 > c1 ? c1 : l0;
+  c0 = h0;
+  c1 = h1;
+  c2 = l1 > c2 ? l1 : c2;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t hi = (uint32_t)__shfl_xor((int)(k >> 32), o, 64), lo = (uint32_t)__shfl_xor((int)(uint32_t)k, o, 64);
+    const uint64_t ok = ((uint64_t)hi << 32) | lo;
+    k = ok > k ? ok : k;
+  }
+  return k;
+}
+
 __global__ __launch_bounds__(ST) void beam_logprobs_kernel(kw_beam_logprobs_args a) {
   __shared__ float shf[ST / 64];
   __shared__ int shi[ST / 64][2];
@@ -181,7 +211,6 @@ __device__ __forceinline__ float bl_sum(float v, float* sh) {
 }
 
 __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logprobs_args a) {
-  __shared__ float shf[BT_S / 64];
   __shared__ int shi[2 * (BT_S / 64)];
   __shared__ RowState st_sh;
   __shared__ float pub[BPART];
@@ -225,23 +254,14 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
   }
   __syncthreads();
   const RowState st = st_sh;
-  // log_softmax normaliser pieces over the RAW slice
-  float mr = -INFINITY;
-#pragma unroll
-  for (int u = 0; u < BUNR; ++u) mr = fmaxf(mr, xv[u]);
-  mr = bl_max(mr, shf);
-  float sr = 0.f;
-#pragma unroll
-  for (int u = 0; u < BUNR; ++u)
-    if (v0 + tid + u * BT_S < v1) sr += expf(xv[u] - mr);
-  sr = bl_sum(sr, shf);
   // processed scores (raw-logit space; every processor is shift invariant) and their statistics
   float sv[BUNR];
-  float mt = -INFINITY, ms = -INFINITY;
-  int it = 0x7fffffff, is = 0x7fffffff, dummy = 0;
+  float mr = -INFINITY, mt = -INFINITY, ms = -INFINITY;
+  int it = 0x7fffffff, is = 0x7fffffff;
 #pragma unroll
   for (int u = 0; u < BUNR; ++u) {
     const int v = v0 + tid + u * BT_S;
+    mr = fmaxf(mr, xv[u]);
     sv[u] = v < v1 ? process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, xv[u]) : -INFINITY;
     if (v < v1) {
       if (v < st.ts_begin) {
@@ -249,93 +269,123 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
       } else if (better(sv[u], v, ms, is)) { ms = sv[u]; is = v; }
     }
   }
-  float sa = 0.f, sts = 0.f, mall = -INFINITY;
-  if (st.rt) {
-    bl_argmax(mt, it, dummy, shf, shi);
-    bl_argmax(ms, is, dummy, shf, shi);
-    mall = fmaxf(mt, ms);
-    if (mall > -INFINITY) {
+  // one workgroup round for the three maxima (the raw maximum of the log_softmax normaliser; the best
+  // text and timestamp scores as 64-bit keys), one for the three sums
+  __shared__ float rmx[BT_S / 64];
+  __shared__ uint64_t rkt[BT_S / 64], rks[BT_S / 64];
+  __shared__ float rsum[3][BT_S / 64];
+  {
+    mr = wave_max(mr);
+    uint64_t kt = 0, ks = 0;
+    if (st.rt) {
+      kt = wave_max_u64(bkey(mt, it));
+      ks = wave_max_u64(bkey(ms, is));
+    }
+    if ((tid & 63) == 0) { rmx[tid >> 6] = mr; rkt[tid >> 6] = kt; rks[tid >> 6] = ks; }
+    __syncthreads();
+    mr = rmx[0];
+    kt = rkt[0];
+    ks = rks[0];
+    for (int w = 1; w < BT_S / 64; ++w) {
+      mr = fmaxf(mr, rmx[w]);
+      kt = rkt[w] > kt ? rkt[w] : kt;
+      ks = rks[w] > ks ? rks[w] : ks;
+    }
+    if (st.rt) {
+      mt = bkey_val(kt); it = bkey_idx(kt);
+      ms = bkey_val(ks); is = bkey_idx(ks);
+    }
+  }
+  float sr = 0.f, sa = 0.f, sts = 0.f, mall = -INFINITY;
+  if (st.rt) mall = fmaxf(mt, ms);
 #pragma unroll
-      for (int u = 0; u < BUNR; ++u) {
-        const int v = v0 + tid + u * BT_S;
-        if (v < v1 && sv[u] > -INFINITY) {
-          sa += expf(sv[u] - mall);
-          if (v >= st.ts_begin) sts += expf(sv[u] - ms);
-        }
+  for (int u = 0; u < BUNR; ++u) {
+    const int v = v0 + tid + u * BT_S;
+    if (v < v1) {
+      sr += expf(xv[u] - mr);
+      if (mall > -INFINITY && sv[u] > -INFINITY) {
+        sa += expf(sv[u] - mall);
+        if (v >= st.ts_begin) sts += expf(sv[u] - ms);
       }
     }
-    sa = bl_sum(sa, shf);
-    sts = bl_sum(sts, shf);
+  }
+  {
+    sr = wave_sum(sr);
+    sa = wave_sum(sa);
+    sts = wave_sum(sts);
+    if ((tid & 63) == 0) { rsum[0][tid >> 6] = sr; rsum[1][tid >> 6] = sa; rsum[2][tid >> 6] = sts; }
+    __syncthreads();
+    sr = sa = sts = 0.f;
+    for (int w = 0; w < BT_S / 64; ++w) {
+      sr += rsum[0][w];
+      sa += rsum[1][w];
+      sts += rsum[2][w];
+    }
   }
   // the slice's KP best processed scores (all tokens; and timestamps only, for the text-ban case):
   // each wave takes its own kp best by shuffle-only rounds (no workgroup barrier per round), then wave 0
   // takes the slice's kp best of the waves' 8 x kp
   const int kp = min(K + 4, KP);
   const int lane = tid & 63, wv = tid >> 6;
-  __shared__ float wcv[2][BT_S / 64][KP];
-  __shared__ int wci[2][BT_S / 64][KP];
+  __shared__ uint64_t wck[2][BT_S / 64][KP];
 #ifdef KW_BEAM_LAB_SKIP_TOPK
   const int nlist = 0;  // lab: time the kernel without the slice top-k
 #else
-  const int nlist = st.rt ? 2 : 1;
+  // timestamp tokens sit at the top of the vocabulary: only the slices holding some need the second list
+  const int nlist = (st.rt && v1 > st.ts_begin) ? 2 : 1;
 #endif
   for (int list = 0; list < nlist; ++list) {
-    unsigned taken = 0;
-    for (int j = 0; j < kp; ++j) {
-      float bv = -INFINITY;
-      int bi = 0x7fffffff, bu = -1;
+    // each lane keeps its 3 best keys below ``floor`` (the last key it gave up), refilled from its 16
+    // registers in the rare round that empties it; a round is one wave max of the lanes' heads
+    uint64_t c0 = 0, c1 = 0, c2 = 0, floor = ~0ull;
+    auto fill = [&]() {
+      c0 = c1 = c2 = 0;
 #pragma unroll
       for (int u = 0; u < BUNR; ++u) {
         const int v = v0 + tid + u * BT_S;
-        if (v < v1 && !(taken >> u & 1) && (list == 0 || v >= st.ts_begin) && better(sv[u], v, bv, bi)) {
-          bv = sv[u]; bi = v; bu = u;
-        }
+        const uint64_t k = (v < v1 && (list == 0 || v >= st.ts_begin)) ? bkey(sv[u], v) : 0;
+        if (k < floor) bins3(k, c0, c1, c2);
       }
-      float gv = bv;
-      int gi = bi, gl = lane;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float ov = __shfl_xor(gv, o, 64);
-        const int oi = __shfl_xor(gi, o, 64), ol = __shfl_xor(gl, o, 64);
-        if (better(ov, oi, gv, gi)) { gv = ov; gi = oi; gl = ol; }
+    };
+    fill();
+    for (int j = 0; j < kp; ++j) {
+      const uint64_t g = wave_max_u64(c0);
+      if (lane == 0) wck[list][wv][j] = g;
+      bool need = false;
+      if (g != 0 && c0 == g) {
+        floor = g;
+        c0 = c1; c1 = c2; c2 = 0;
+        need = c0 == 0;
       }
-      if (lane == gl && bu >= 0 && gi == bi) taken |= 1u << bu;
-      if (lane == 0) { wcv[list][wv][j] = gv; wci[list][wv][j] = gi; }
+      if (__ballot(need)) {
+        if (need) fill();
+      }
     }
   }
   __syncthreads();
   if (wv == 0) {
-    for (int list = 0; list < nlist; ++list) {
-      // lane l holds candidates l and l + 64 of the waves' 8 x kp (kp <= 20: 160 <= 128 + 32 ... two slots)
-      float c0 = -INFINITY, c1 = -INFINITY;
-      int i0 = 0x7fffffff, i1 = 0x7fffffff;
+    for (int list = 0; list < 2; ++list) {
+      if (list >= nlist) {  // (no timestamp tokens in this slice: an empty list)
+        if (lane < kp) {
+          pub[9 + list * 2 * KP + 2 * lane] = -INFINITY;
+          pub[9 + list * 2 * KP + 2 * lane + 1] = __int_as_float(0x7fffffff);
+        }
+        continue;
+      }
+      // the waves' 8 x kp keys (kp <= KP: at most 3 per lane), then kp rounds of a wave max
+      uint64_t c0 = 0, c1 = 0, c2 = 0;
       const int n = (BT_S / 64) * kp;
-      if (lane < n) { c0 = wcv[list][lane / kp][lane % kp]; i0 = wci[list][lane / kp][lane % kp]; }
-      if (lane + 64 < n) { c1 = wcv[list][(lane + 64) / kp][(lane + 64) % kp]; i1 = wci[list][(lane + 64) / kp][(lane + 64) % kp]; }
-      float c2 = -INFINITY;
-      int i2 = 0x7fffffff;
-      if (lane + 128 < n) { c2 = wcv[list][(lane + 128) / kp][(lane + 128) % kp]; i2 = wci[list][(lane + 128) / kp][(lane + 128) % kp]; }
-      for (int j = 0; j < kp; ++j) {
-        float bv = c0;
-        int bi = i0, bs = 0;
-        if (better(c1, i1, bv, bi)) { bv = c1; bi = i1; bs = 1; }
-        if (better(c2, i2, bv, bi)) { bv = c2; bi = i2; bs = 2; }
-        float gv = bv;
-        int gi = bi, gl = lane;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const float ov = __shfl_xor(gv, o, 64);
-          const int oi = __shfl_xor(gi, o, 64), ol = __shfl_xor(gl, o, 64);
-          if (better(ov, oi, gv, gi)) { gv = ov; gi = oi; gl = ol; }
-        }
-        if (lane == gl) {
-          if (bs == 0) { c0 = -INFINITY; i0 = 0x7fffffff; }
-          else if (bs == 1) { c1 = -INFINITY; i1 = 0x7fffffff; }
-          else { c2 = -INFINITY; i2 = 0x7fffffff; }
-        }
+      for (int t = 0; t < 3; ++t) {
+        const int e = lane + 64 * t;
+        if (e < n) bins3(wck[list][e / kp][e % kp], c0, c1, c2);
+      }
+      for (int j = 0; j < kp; ++j) {
+        const uint64_t g = wave_max_u64(c0);
+        if (g != 0 && c0 == g) { c0 = c1; c1 = c2; c2 = 0; }
         if (lane == 0) {
-          pub[9 + list * 2 * KP + 2 * j] = gv;
-          pub[9 + list * 2 * KP + 2 * j + 1] = __int_as_float(gi);
+          pub[9 + list * 2 * KP + 2 * j] = g ? bkey_val(g) : -INFINITY;
+          pub[9 + list * 2 * KP + 2 * j + 1] = __int_as_float(g ? bkey_idx(g) : 0x7fffffff);
         }
       }
     }

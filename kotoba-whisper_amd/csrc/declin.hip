@@ -24,6 +24,8 @@
 // Everything is bitwise deterministic: no float atomics, every reduction in a fixed order.
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "kw_common.h"
 
 // development hooks (tools/lab/declin_lab.hip records s_memrealtime stamps through them); no-ops here
@@ -339,6 +341,171 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
   KW_DEC_STAMP_FLUSH
 }
 
+// More than 32 rows without a K split (prefill positions, beam rows): each workgroup keeps its
+// columns' weight fragments in registers and walks ``zper`` 32-row chunks.  (One z-slice per chunk
+// re-streams the weights per chunk and runs as many rounds of workgroups as there are chunks, each a
+// full load round trip: 50 us for fc1 at 320 rows.)  Per chunk the arithmetic is dec_linear_kernel's
+// operation for operation -- the same fragments, MFMA order, wave-ordered reduction and epilogue --
+// so results are bitwise those of the chunked launch.
+template <int KTM, int NCB, bool LNA, int EPI, typename TC>
+__global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) {
+  __shared__ f32x4 red[MAXW][NCB][2][64];
+  __shared__ float rpart[MAXW][32][2];
+  __shared__ float rstat[32][2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int cg = blockIdx.x;
+  const int nkt = p.K >> 5;
+  const int kt0 = (nkt * wave) / nw, kt1 = (nkt * (wave + 1)) / nw;  // <= KTM (host-checked)
+  const int ktl = max(kt1 - 1, kt0);
+  const int arow = lane & 15, akoff = 8 * (lane >> 4);
+  const int nz = (p.M + 31) / 32;
+  const int z0 = blockIdx.z * zper, z1 = min(nz, z0 + zper);
+  bf16x8 w[NCB][KTM];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c)
+#pragma unroll
+    for (int u = 0; u < KTM; ++u)
+      w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)(cg * NCB + c) * nkt + min(kt0 + u, ktl)) * 64 + lane);
+  float ebias[NCB], ecsum[NCB];
+#pragma unroll
+  for (int c = 0; c < NCB; ++c) {
+    const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
+    ebias[c] = p.bias ? p.bias[n] : 0.f;
+    ecsum[c] = LNA ? p.ln_colsum[n] : 0.f;
+  }
+  for (int z = z0; z < z1; ++z) {
+    const int m0 = 32 * z, M = min(32, p.M - m0);
+    const bf16_t* x = p.x + (int64_t)m0 * p.ldx;
+    bf16x8 a0[KTM], a1[KTM];
+    {
+      const int r0 = min(arow, M - 1), r1 = min(16 + arow, M - 1);
+#pragma unroll
+      for (int u = 0; u < KTM; ++u) {
+        const int k = min(kt0 + u, ktl) * 32 + akoff;
+        a0[u] = *reinterpret_cast<const bf16x8*>(x + (int64_t)r0 * p.ldx + k);
+        a1[u] = *reinterpret_cast<const bf16x8*>(x + (int64_t)r1 * p.ldx + k);
+      }
+    }
+    float hold[NCB][2][4];
+    if constexpr (EPI == KW_EPI_RESID) {
+      if (wave == 0) {
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = min(16 * hh + 4 * (lane >> 4) + r, M - 1);
+              hold[c][hh][r] = p.h[(int64_t)(m0 + m) * p.ldh + n];
+            }
+        }
+      }
+    }
+    f32x4 c0[NCB], c1[NCB];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      c0[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+      c1[c] = c0[c];
+    }
+#pragma unroll
+    for (int u = 0; u < KTM; ++u) {
+      if (kt0 + u < kt1) {
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          c0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], w[c][u], c0[c], 0, 0, 0);
+          c1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[c][u], c1[c], 0, 0, 0);
+        }
+      }
+    }
+    if constexpr (LNA) {  // row statistics on the matrix cores, as dec_linear_kernel step 3
+      bf16x8 ones;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+      f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0, q0 = s0, q1 = s0;
+#pragma unroll
+      for (int u = 0; u < KTM; ++u)
+        if (kt0 + u < kt1) {
+          s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], ones, s0, 0, 0, 0);
+          s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], ones, s1, 0, 0, 0);
+          q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], a0[u], q0, 0, 0, 0);
+          q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], a1[u], q1, 0, 0, 0);
+        }
+      if ((lane & 15) == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          rpart[wave][4 * (lane >> 4) + i][0] = s0[i];
+          rpart[wave][16 + 4 * (lane >> 4) + i][0] = s1[i];
+        }
+      }
+      const int di = (lane & 15) - 4 * (lane >> 4);
+      if (di >= 0 && di < 4) {
+        rpart[wave][lane & 15][1] = q0[di];
+        rpart[wave][16 + (lane & 15)][1] = q1[di];
+      }
+    }
+    if (nw > 1) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        red[wave][c][0][lane] = c0[c];
+        red[wave][c][1][lane] = c1[c];
+      }
+    }
+    __syncthreads();
+    if (wave == 0) {
+      for (int w2 = 1; w2 < nw; ++w2)
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) {
+          c0[c] += red[w2][c][0][lane];
+          c1[c] += red[w2][c][1][lane];
+        }
+      if constexpr (LNA) {
+        if (lane < 32) {
+          float sx = 0.f, sq = 0.f;
+          for (int w2 = 0; w2 < nw; ++w2) {
+            sx += rpart[w2][lane][0];
+            sq += rpart[w2][lane][1];
+          }
+          const float inv = 1.f / (float)p.K;
+          const float mean = sx * inv;
+          rstat[lane][0] = mean;
+          rstat[lane][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + p.ln_eps);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        const int n = (cg * NCB + c) * 16 + (lane & 15);
+        const bool nvalid = n < p.N;
+        const float bn = ebias[c];
+        const float cs = ecsum[c];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = 16 * hh + 4 * (lane >> 4) + r;
+            const bool valid = nvalid && m < M;
+            float v = hh ? c1[c][r] : c0[c][r];
+            if constexpr (LNA) v = rstat[m][1] * (v - rstat[m][0] * cs);
+            v += bn;
+            if constexpr (EPI == KW_EPI_RESID) {
+              v += hold[c][hh][r];
+              if (valid) {
+                p.h[(int64_t)(m0 + m) * p.ldh + n] = v;
+                p.hb[(int64_t)(m0 + m) * p.ldh + n] = f2bf(v);
+              }
+            } else {
+              if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
+              if (n < p.scale_cols) v *= p.scale;
+              if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)(m0 + m) * p.ldc + n, v);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();  // red / rpart / rstat are rewritten by the next chunk
+  }
+}
+
 // LM head (proj_out with the final LayerNorm folded, modeling_whisper.py:790,1080) as a persistent
 // weight stream: the generic kernel above re-reads the 32 activation rows from L2 in every one of its
 // 1,621 workgroups (as many L2 bytes as weight bytes) and runs 1.6 rounds of them.  Here each of
@@ -524,9 +691,28 @@ Geo choose(int64_t N, int64_t K) {
 bool use_xlds(int64_t N, const Geo& g) { return g.ks == 1 && (N + 16 * g.ncb - 1) / (16 * g.ncb) <= 256; }
 size_t x_lds_bytes_for(int nkt, bool xlds) { return xlds ? x_lds_bytes(nkt) : 0; }
 
+int device_cus() {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
+  return ncu;
+}
+
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
 hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
   const int nkt = p.K / 32;
+  if (g.ks == 1 && p.M > 32) {  // many rows: weight-stationary workgroups over row chunks
+    const int ncg = (p.N + 16 * NCB - 1) / (16 * NCB), nz = (p.M + 31) / 32;
+    const int zg0 = std::max(1, std::min(nz, (2 * device_cus()) / ncg));
+    const int zper = (nz + zg0 - 1) / zg0, zg = (nz + zper - 1) / zper;
+    hipLaunchKernelGGL((dec_linear_rows_kernel<KTM, NCB, LNA, EPI, TC>), dim3((unsigned)ncg, 1, (unsigned)zg),
+                       dim3((unsigned)(64 * g.nw)), 0, s, p, zper);
+    return hipGetLastError();
+  }
   const size_t shm = x_lds_bytes_for(nkt, p.xlds);
   static size_t attr = 0;  // dynamic LDS this instantiation is cleared for
   if (shm > attr) {

@@ -366,7 +366,7 @@ def test_cross_attn_step(dtype, q_len, S):
     torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
 
 
-@pytest.mark.parametrize("q_len", [2, 4, 5, 20])
+@pytest.mark.parametrize("q_len", [2, 3, 4, 5, 8, 13, 20])
 @pytest.mark.parametrize("S", [1500, 200])
 def test_cross_attn_multirow_bitwise(q_len, S):
     """bf16 rows of one item sharing a K/V pass (prefill positions, beams) == each row attended alone by
@@ -519,6 +519,42 @@ def test_dec_linear_layernorm(M, N, K):
     torch.testing.assert_close(C, _ref_gemm(xn, W, bias), atol=4e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("M", [64, 70, 320])
+@pytest.mark.parametrize("N,K,mode", [(3840, 1280, "ln"), (1280, 1280, "resid"), (5120, 1280, "gelu_bf16"),
+                                      (1152, 384, "ln"), (384, 1536, "resid")])
+def test_dec_linear_rows_bitwise(M, N, K, mode):
+    """More than 32 rows (prefill, beam rows) run weight-stationary workgroups over 32-row chunks: bit for
+    bit the results of the same linear launched on each 32-row slice alone."""
+    torch.manual_seed(M + N + K)
+    x = (torch.randn(M, K, device="cuda") * 2 + 0.3).bfloat16()
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    Wp = ops.pack_weight(W)
+    b = torch.randn(N, device="cuda")
+    ws = torch.zeros(ops.dec_linear_workspace_bytes(N, K) // 4 + 1, device="cuda")
+    h0 = torch.randn(M, N, device="cuda")
+
+    def run(rows, r0):
+        xs = x[r0:r0 + rows].contiguous()
+        if mode == "resid":
+            h = h0[r0:r0 + rows].clone()
+            hb = torch.empty(rows, N, device="cuda", dtype=torch.bfloat16)
+            ops.DecLinearPlan(xs, Wp, rows, N, K, bias=b, resid=(h, hb, N, 0), workspace=ws)()
+            return h, hb
+        if mode == "ln":
+            C = torch.empty(rows, N, device="cuda")
+            ops.DecLinearPlan(xs, Wp, rows, N, K, ln=(1e-5, ops.ln_colsum(W)), bias=b, C=C)()
+            return (C,)
+        C = torch.empty(rows, N, device="cuda", dtype=torch.bfloat16)
+        ops.DecLinearPlan(xs, Wp, rows, N, K, bias=b, C=C, gelu=True, scale=0.5, scale_cols=N // 3)()
+        return (C,)
+
+    full = run(M, 0)
+    for r0 in range(0, M, 32):
+        part = run(min(32, M - r0), r0)
+        for f, q in zip(full, part):
+            assert torch.equal(f[r0:r0 + q.shape[0]], q), r0
+
+
 @pytest.mark.parametrize("M", [32, 5, 70, 300])
 @pytest.mark.parametrize("N,K", [(1280, 1280), (1280, 5120), (384, 1536)])
 def test_dec_linear_resid(M, N, K):
@@ -555,10 +591,14 @@ def test_embed_mirror():
 
 
 @pytest.mark.parametrize("rt", [False, True])
-@pytest.mark.parametrize("R,V,k,n_hist", [(10, 51865, 10, 0), (10, 51865, 10, 5), (40, 51866, 6, 3), (4, 900, 16, 2)])
-def test_beam_logprobs_split_rows(rt, R, V, k, n_hist):
+@pytest.mark.parametrize("R,V,k,n_hist,adv", [(10, 51865, 10, 0, False), (10, 51865, 10, 5, False),
+                                              (40, 51866, 6, 3, False), (4, 900, 16, 2, False),
+                                              (12, 51866, 10, 2, True)])
+def test_beam_logprobs_split_rows(rt, R, V, k, n_hist, adv):
     """kw_beam_logprobs split over 8 workgroups per row == the one-workgroup kernel: the same k candidate
-    tokens per row in the same order, log-probs equal up to the normaliser's summation order."""
+    tokens per row in the same order, log-probs equal up to the normaliser's summation order.  ``adv``:
+    logits on a 0.5 grid (ties broken by token), +-0.0 values, and rows whose best tokens all sit in one
+    thread's registers of one slice (a lane that wins more rounds than its 3-key cache holds)."""
     import ctypes
 
     from kwhisper import _lib as L
@@ -581,6 +621,14 @@ def test_beam_logprobs_split_rows(rt, R, V, k, n_hist):
     done = torch.zeros(1, dtype=torch.int32, device="cuda")
     x = (rng.standard_normal((R, V)) * 3).astype(np.float32)
     x[::2, ts_begin:] += 3.0
+    if adv:
+        x = np.round(x * 2) / 2
+        x[:, 5:40:3] = -0.0
+        per = (V + 7) // 8
+        for r in range(R):  # slice r % 8, thread 17: tokens v0 + 17 + 512 u
+            v0 = (r % 8) * per
+            toks = [v0 + 17 + 512 * u for u in range(16) if v0 + 17 + 512 * u < min(V, v0 + per)]
+            x[r, toks] = 30.0 - (np.arange(len(toks)) % 3)
     lg = torch.from_numpy(x).cuda()
     res = []
     for split in (False, True):
