@@ -635,8 +635,9 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
     float sc[4][8];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      if (r0 + r >= nq) break;  // (uniform: rows past the group's last are neither computed nor read)
       float qv[8];
-      load8<T>(q + ((int64_t)(b * q_len + qi0 + min(r0 + r, nq - 1))) * H * HD + h * HD + sub * 8, qv);
+      load8<T>(q + ((int64_t)(b * q_len + qi0 + r0 + r)) * H * HD + h * HD + sub * 8, qv);
       float mx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -657,6 +658,7 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      if (r0 + r >= nq) break;
       const float m = fmaxf(fmaxf(stat[r][0], stat[r][1]), fmaxf(stat[r][2], stat[r][3]));
       mrow[r0 + r] = m;
       float lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};

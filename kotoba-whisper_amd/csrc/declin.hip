@@ -512,6 +512,9 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
 // ~256 workgroups loads its waves' activation fragments and the rows' LayerNorm statistics ONCE, then
 // walks a contiguous run of column groups (2 x 16 columns each) with the next group's weights in
 // flight while the current one is reduced across waves and written (fixed-order sums: deterministic).
+#ifndef KW_LMH_MAX_ROWS
+#define KW_LMH_MAX_ROWS 32  // (lab knob: rows up to which the LM head takes lm_head_kernel)
+#endif
 constexpr int LMH_KTM = 5;   // k-tiles per wave
 constexpr int LMH_NCB = 2;   // column blocks per group
 
@@ -776,8 +779,9 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   // LM head: LayerNorm-fused, f32 logits, a wide N and a short K -> the persistent weight stream
+  // (more rows than one chunk: the weight-stationary rows kernel instead, which streams the weights once)
   const bool lmh = a->ln && a->epilogue == KW_EPI_STORE && a->c_dtype == KW_DT_F32 && a->N >= 8192 &&
-                   (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && !a->gelu && a->scale_cols == 0;
+                   (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && !a->gelu && a->scale_cols == 0 && a->M <= KW_LMH_MAX_ROWS;
   // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each)
   const int64_t step = (g.ks == 1 || lmh) ? a->M : 32 * ZMAX;
   for (int64_t m0 = 0; m0 < a->M; m0 += step) {
