@@ -765,6 +765,215 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
   }
 }
 
+// Cross-attention for up to 32 query rows of one item on the matrix cores (beam rows, the beam
+// prefill's P x beams positions): the encoder kernel's scheme -- S^T = K Q^T on v_mfma_f32_32x32x16_bf16,
+// O^T = V^T P^T with P^T straight from the accumulators and V^T by ds_read_b64_tr_b16 -- on one 64-key
+// tile per wave.  The 4 waves of a workgroup cover one <= 256-key chunk with a common row maximum
+// (exchanged through LDS) and sum their (l, O) in wave order; the chunks combine as cross_attn_kernel's
+// (write-through partials, the last arriver merges in chunk order).  P enters the matrix cores in bf16
+// (the one-row kernel keeps it f32): rows agree with it to bf16 rounding, not bitwise.
+#ifndef KW_CROSS_MFMA_MIN_Q
+#define KW_CROSS_MFMA_MIN_Q 5  // (lab knob: rows per item from which the MFMA kernel takes over)
+#endif
+constexpr int XM_LDS = 4 * TILE_BYTES;  // per wave: its K, then V, image (32 KB); reused for the (l, O) merge
+
+__global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __restrict__ q, int q_len, int H,
+                                                              const bf16_t* __restrict__ kc,
+                                                              const bf16_t* __restrict__ vc, int S, int chunk,
+                                                              float* __restrict__ ws, int* __restrict__ cnt,
+                                                              bf16_t* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) char xsm[];
+  __shared__ float wmax[4][32], wsum[4][32];
+  __shared__ int last;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int hh = lane >> 5, ql = lane & 31;
+  const int ngrp = (q_len + 31) / 32;
+  const int h = blockIdx.x % H;
+  const int bg = blockIdx.x / H;
+  const int b = bg / ngrp, qi0 = (bg - b * ngrp) * 32;
+  const int nq = min(32, q_len - qi0);
+  const int split = blockIdx.y, ns = gridDim.y;
+  const int k0 = split * chunk, k1 = min(S, k0 + chunk);
+  const int kt0 = k0 + 64 * wave;  // this wave's tile (keys past k1 are masked)
+  const bf16_t* K = kc + ((int64_t)b * H + h) * S * HD;
+  const bf16_t* V = vc + ((int64_t)b * H + h) * S * HD;
+  // one 8-KB LDS image per wave: K lands there by LDS-DMA; V (loaded at the same time, into registers,
+  // 16 B per lane per 8-row group) is written over it once the scores are computed
+  char* kb = xsm + wave * TILE_BYTES;
+  u32x4 vreg[8];
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {  // 64 rows x 128 B, XOR-swizzled as the encoder's K / V images
+    const int row = 8 * g + (lane >> 3);
+    const int key = min(kt0 + row, k1 - 1);
+    const int slot = lane & 7;
+    glds16(K + (int64_t)key * HD + (slot ^ ((row >> 1) & 7)) * 8, kb + g * 1024);
+    vreg[g] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(V + (int64_t)key * HD + slot * 8));
+  }
+  // Q fragments (B operand of S^T = K Q^T): lane holds Q[row ql][16s + 8hh .. +7]
+  bf16x8 qf[4];
+  {
+    const bf16_t* qr = q + (int64_t)(b * q_len + qi0 + min(ql, nq - 1)) * H * HD + h * HD;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qr + 16 * s + 8 * hh);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  f32x16 st[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[i][r] = 0.f;
+    const int row = i * 32 + ql;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int c = 2 * s + hh;
+      const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + row * 128 + ((c ^ ((row >> 1) & 7)) << 4));
+      st[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[i], 0, 0, 0);
+    }
+  }
+  // the wave's K image is consumed (its fragment reads completed before the MFMAs): V over it, in the
+  // transposed-read swizzle (LDS ops of one wave complete in order)
+  char* vb = kb;
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    const int row = 8 * g + (lane >> 3), slot = lane & 7;
+    *reinterpret_cast<u32x4*>(vb + row * 128 + ((slot ^ (((row >> 1) & 1) << 2)) << 4)) = vreg[g];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // S^T layout: lane holds query ql, keys i*32 + (r&3) + 8*(r>>2) + 4*hh
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kt0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (key >= k1) st[i][r] = -INFINITY;
+      mx = fmaxf(mx, st[i][r]);
+    }
+  mx = xor32_max(mx);
+  if (hh == 0) wmax[wave][ql] = mx;
+  __syncthreads();
+  const float m = fmaxf(fmaxf(wmax[0][ql], wmax[1][ql]), fmaxf(wmax[2][ql], wmax[3][ql]));
+  const float mneg = -m * LOG2E;
+  float rs = 0.f;
+  bf16x8 pf[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(st[i][8 * s + e], LOG2E, mneg));
+        rs += p;
+        pf[i][s][e] = (__bf16)p;
+      }
+  rs = xor32_sum(rs);
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  {
+    const int li = lane & 15, qq = li >> 2, pp = li & 3, grp = (lane >> 4) & 1;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int i = n >> 1, s = n & 1;
+      v2u32 t[2][2];
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          const int row = i * 32 + 16 * s + 8 * half + 4 * hh + qq;
+          const int ch = db * 4 + 2 * grp + (pp >> 1);
+          const int off = row * 128 + ((ch ^ (((row >> 1) & 1) << 2)) << 4) + (pp & 1) * 8;
+          asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(t[db][half]) : "v"(lds_u32(vb + off)));
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t[0][0]), "+v"(t[0][1]), "+v"(t[1][0]), "+v"(t[1][1]));
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const v4u32 w = {t[db][0][0], t[db][0][1], t[db][1][0], t[db][1][1]};
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), pf[i][s], o[db], 0, 0, 0);
+      }
+    }
+  }
+  // merge the waves: l and O^T (dims db*32 + (r&3) + 8*(r>>2) + 4*hh of query ql) summed in wave order
+  if (hh == 0) wsum[wave][ql] = rs;
+  __syncthreads();  // every wave is past its tile reads: the K/V images become the merge buffer
+  float* mo = reinterpret_cast<float*>(xsm);  // [wave][query 32][dim 64]
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mo[(wave * 32 + ql) * HD + db * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh] = o[db][r];
+  __syncthreads();
+  // thread (query tq, 8 dims from td): the chunk's (m, l, o) of its row
+  const int tq = tid >> 3, td = (tid & 7) * 8;
+  const bool mine = tq < nq;
+  const float mq = fmaxf(fmaxf(wmax[0][tq], wmax[1][tq]), fmaxf(wmax[2][tq], wmax[3][tq]));
+  const float lq = ((wsum[0][tq] + wsum[1][tq]) + wsum[2][tq]) + wsum[3][tq];
+  float ov[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e)
+    ov[e] = ((mo[(0 * 32 + tq) * HD + td + e] + mo[(1 * 32 + tq) * HD + td + e]) + mo[(2 * 32 + tq) * HD + td + e]) +
+            mo[(3 * 32 + tq) * HD + td + e];
+  const int row = (b * q_len + qi0 + min(tq, nq - 1)) * H + h;
+  bf16_t* orow = out + (int64_t)(b * q_len + qi0 + min(tq, nq - 1)) * H * HD + h * HD + td;
+  if (ns == 1) {
+    if (mine) {
+      const float inv = 1.f / lq;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) orow[e] = f2bf(ov[e] * inv);
+    }
+    return;
+  }
+  float* part = ws + (int64_t)row * ns * (HD + 2);
+  if (mine) {
+    float* w = part + (int64_t)split * (HD + 2);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) __hip_atomic_store(w + 2 + td + e, ov[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (td == 0) {
+      __hip_atomic_store(w, mq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(w + 1, lq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* c = cnt + (b * q_len + qi0) * H + h;  // one counter per row group
+  if (tid == 0) {
+    const int prev = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == ns - 1;
+    if (prev == ns - 1) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if (!last || !mine) return;
+  constexpr int NSMAX = 8;
+  float ms[NSMAX], ls[NSMAX];
+#pragma unroll
+  for (int qq2 = 0; qq2 < NSMAX; ++qq2) {
+    ms[qq2] = qq2 < ns ? __hip_atomic_load(part + qq2 * (HD + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -INFINITY;
+    ls[qq2] = qq2 < ns ? __hip_atomic_load(part + qq2 * (HD + 2) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+  }
+  float M = -INFINITY;
+#pragma unroll
+  for (int qq2 = 0; qq2 < NSMAX; ++qq2)
+    if (qq2 < ns) M = fmaxf(M, ms[qq2]);
+  float f[NSMAX], lt = 0.f;
+#pragma unroll
+  for (int qq2 = 0; qq2 < NSMAX; ++qq2) {
+    f[qq2] = qq2 < ns ? expf(ms[qq2] - M) : 0.f;
+    if (qq2 < ns) lt = fmaf(ls[qq2], f[qq2], lt);
+  }
+  const float inv = 1.f / lt;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float ot = 0.f;
+#pragma unroll
+    for (int qq2 = 0; qq2 < NSMAX; ++qq2)
+      if (qq2 < ns) ot = fmaf(__hip_atomic_load(part + qq2 * (HD + 2) + 2 + td + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), f[qq2], ot);
+    orow[e] = f2bf(ot * inv);
+  }
+}
+
 // decoder self-attention for one new position (q_len == 1): split 0 appends k/v at L-1; each split
 // attends over its <= 256-key chunk of [0, L) (the new row read from qkv, never from the cache in the
 // same launch); splits beyond L exit; the last arriving split combines.
@@ -905,7 +1114,18 @@ extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q
     const dim3 gm((unsigned)(B * H), (unsigned)ns);
     hipLaunchKernelGGL((cross_attn_multi_kernel<bf16_t, 4>), gm, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
-  } else if (dtype == KW_DT_BF16 && q_len > 4) {  // up to 8 rows per K/V pass (beam 5-8), groups of 8 beyond
+  } else if (dtype == KW_DT_BF16 && q_len >= KW_CROSS_MFMA_MIN_Q) {  // beams: up to 32 rows per pass, MFMA
+    static bool attr = false;
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&cross_attn_mfma_kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, XM_LDS);
+      if (e != hipSuccess) return kw_set_error(e);
+      attr = true;
+    }
+    const dim3 gm((unsigned)(B * ((q_len + 31) / 32) * H), (unsigned)ns);
+    hipLaunchKernelGGL(cross_attn_mfma_kernel, gm, dim3(256), XM_LDS, s, (const bf16_t*)q, (int)q_len, (int)H,
+                       (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
+  } else if (dtype == KW_DT_BF16 && q_len > 4) {  // up to 8 rows per K/V pass, groups of 8 beyond
     const dim3 gm((unsigned)(B * ((q_len + 7) / 8) * H), (unsigned)ns);
     hipLaunchKernelGGL((cross_attn_multi_kernel<bf16_t, 8>), gm, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);

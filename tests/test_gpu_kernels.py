@@ -366,11 +366,12 @@ def test_cross_attn_step(dtype, q_len, S):
     torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
 
 
-@pytest.mark.parametrize("q_len", [2, 3, 4, 5, 8, 13, 20])
+@pytest.mark.parametrize("q_len", [2, 3, 4, 5, 8, 13, 20, 32, 45])
 @pytest.mark.parametrize("S", [1500, 200])
 def test_cross_attn_multirow_bitwise(q_len, S):
     """bf16 rows of one item sharing a K/V pass (prefill positions, beams) == each row attended alone by
-    the one-row kernel, bit for bit."""
+    the one-row kernel: bit for bit up to 4 rows (the same f32 arithmetic per row); from 5 rows the matrix-
+    core kernel takes P in bf16, within bf16 rounding (atol 1e-2, rtol 1e-2)."""
     B, H, hd = 3, 20, 64
     d = H * hd
     dtype = torch.bfloat16
@@ -386,7 +387,10 @@ def test_cross_attn_multirow_bitwise(q_len, S):
     qv = q.view(B, q_len, d)
     for i in range(q_len):
         ops.cross_attn_step(qv[:, i].contiguous(), B, 1, H, hd, k, v, S, one, ws1)
-        assert torch.equal(out.view(B, q_len, d)[:, i], one), i
+        if q_len <= 4:
+            assert torch.equal(out.view(B, q_len, d)[:, i], one), i
+        else:
+            torch.testing.assert_close(out.view(B, q_len, d)[:, i].float(), one.float(), atol=1e-2, rtol=1e-2)
 
 
 # ---------------------------------------------------------------- greedy step (processors + argmax)
