@@ -506,6 +506,155 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
   }
 }
 
+// LM head over 33..LMR_MAXROWS rows (beam rows: 64 items x 5 beams = 320) as a GEMM: workgroup = 64
+// columns (one 16-column block per wave, all of K) x ALL rows.  Per k-tile the workgroup stages the
+// rows' 32-wide activation slice in LDS once (LDS-DMA, double-buffered, XOR-swizzled for conflict-free
+// fragment reads) and every wave multiplies it by its one weight fragment (1 KB, streamed once from HBM,
+// the next k-tile's in flight): no cross-wave reduction, no weight re-read per row chunk (the rows
+// kernel re-reads the activations per 32 columns and reduces per chunk: 258 us at 320 rows).  The
+// LayerNorm statistics accumulate from the same LDS slices (f32, k order); epilogue as the folded
+// LayerNorm of dec_linear_kernel.  Results agree with the 32-row kernels to f32 summation order.
+constexpr int LMR_MAXROWS = 320, LMR_NZ = LMR_MAXROWS / 32;
+
+__device__ __forceinline__ bf16x8 lmr_lds_read(const char* p) {
+  // inline asm: a builtin LDS read after an LDS-DMA would get an s_waitcnt vmcnt(0) (the compiler
+  // cannot tell the slice being read from the ones in flight); lmr waits are explicit lgkmcnt counts
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p)
+               : "memory");
+  return v;
+}
+__device__ __forceinline__ void lmr_barrier() {  // raw s_barrier: no implicit vmcnt(0) drain
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int G>  // LDS-DMA pieces per wave per slice (= staged rows / 64)
+__global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
+  constexpr int NBUF = 3, PD = 8;  // activation slices in LDS (2 in flight), weight fragments in flight
+  __shared__ __attribute__((aligned(16))) char abuf[NBUF][LMR_MAXROWS * 64];  // 3 x 20 KB
+  __shared__ float rsum[LMR_MAXROWS], rsq[LMR_MAXROWS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = p.M, nkt = p.K >> 5, nz = (M + 31) / 32;
+  const int n_cb = (p.N + 15) / 16;
+  const int cb = min(blockIdx.x * 4 + wave, n_cb - 1);
+  // staging: piece j (16 B) = row j >> 2, LDS chunk j & 3, holding source chunk (j & 3) ^ ((row >> 2) & 3)
+  auto stage = [&](int buf, int kt) {
+    char* dst = abuf[buf];
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const int j0 = wave * 64 + 256 * i;
+      const int j = j0 + lane, row = j >> 2, ch = (j & 3) ^ ((row >> 2) & 3);
+      glds16(p.x + (int64_t)min(row, M - 1) * p.ldx + kt * 32 + ch * 8, dst + j0 * 16);
+    }
+  };
+  f32x4 acc0[LMR_NZ], acc1[LMR_NZ];
+#pragma unroll
+  for (int z = 0; z < LMR_NZ; ++z) {
+    acc0[z] = f32x4{0.f, 0.f, 0.f, 0.f};
+    acc1[z] = acc0[z];
+  }
+  // row statistics from the fragments: wave w sums chunks z = w, w + 4, w + 8 (slot z >> 2); lane
+  // (fr, fc) holds 8 values of rows 32z + fr and 32z + 16 + fr
+  constexpr int NSL = (LMR_NZ + 3) / 4;
+  float ss[NSL][2], sq[NSL][2];
+#pragma unroll
+  for (int t = 0; t < NSL; ++t) ss[t][0] = ss[t][1] = sq[t][0] = sq[t][1] = 0.f;
+  const bf16x8* W = p.W + (int64_t)cb * nkt * 64 + lane;
+  constexpr int NZ = 2 * G;  // 32-row chunks computed (rows past M are clamped copies, never stored)
+  const int fr = lane & 15, fc = lane >> 4;  // fragment row within a 16-row block, 16-B chunk
+  // Branch-free k loop (the compiler's own vmcnt bookkeeping then stays exact): the slice and weight
+  // prefetches are clamped to the last k-tile instead of skipped.  Issue order: W(0..5), S(0), W(6),
+  // S(1), W(7) | k-tile kt: S(kt+2), W(kt+8); so at the top of k-tile kt exactly W(kt+6), S(kt+1) and
+  // W(kt+7) -- G + 2 operations -- are younger than S(kt).  nkt % PD == 0 (host-checked).
+  bf16x8 wr[PD];
+#pragma unroll
+  for (int u = 0; u < 6; ++u) wr[u] = __builtin_nontemporal_load(W + (int64_t)min(u, nkt - 1) * 64);
+  stage(0, 0);
+  wr[6] = __builtin_nontemporal_load(W + (int64_t)min(6, nkt - 1) * 64);
+  stage(1, min(1, nkt - 1));
+  wr[7] = __builtin_nontemporal_load(W + (int64_t)min(7, nkt - 1) * 64);
+  for (int kb = 0; kb < nkt; kb += PD) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      const int kt = kb + u;
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + 2) : "memory");
+      lmr_barrier();
+      stage((kt + 2) % NBUF, min(kt + 2, nkt - 1));
+      const char* a = abuf[kt % NBUF];
+      bf16x8 fa[2][2];
+      auto rd = [&](int z, bf16x8 (&f)[2]) {
+        const int r0 = 32 * z + fr, r1 = r0 + 16;
+        f[0] = lmr_lds_read(a + r0 * 64 + ((fc ^ ((r0 >> 2) & 3)) << 4));
+        f[1] = lmr_lds_read(a + r1 * 64 + ((fc ^ ((r1 >> 2) & 3)) << 4));
+      };
+      rd(0, fa[0]);
+#pragma unroll
+      for (int z = 0; z < NZ; ++z) {
+        bf16x8(&f)[2] = fa[z & 1];
+        if (z + 1 < NZ) {
+          rd(z + 1, fa[(z + 1) & 1]);
+          asm volatile("s_waitcnt lgkmcnt(2)" : "+v"(f[0]), "+v"(f[1]));
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(f[0]), "+v"(f[1]));
+        }
+        acc0[z] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[0], wr[u], acc0[z], 0, 0, 0);
+        acc1[z] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[1], wr[u], acc1[z], 0, 0, 0);
+        if ((z & 3) == wave) {
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float x = (float)f[hh][e];
+              ss[z >> 2][hh] += x;
+              sq[z >> 2][hh] = fmaf(x, x, sq[z >> 2][hh]);
+            }
+        }
+      }
+      wr[u] = __builtin_nontemporal_load(W + (int64_t)min(kt + PD, nkt - 1) * 64);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the clamped tail prefetches)
+  // finish the statistics: the 4 lanes of a row (fc = 0..3) in chunk order
+#pragma unroll
+  for (int t = 0; t < NSL; ++t) {
+    const int z = wave + 4 * t;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      float a = ss[t][hh], b = sq[t][hh];
+      const float a1 = __shfl_xor(a, 16, 64), b1 = __shfl_xor(b, 16, 64);
+      const float a2 = __shfl_xor(a, 32, 64), b2 = __shfl_xor(b, 32, 64);
+      const float a3 = __shfl_xor(a, 48, 64), b3 = __shfl_xor(b, 48, 64);
+      if (fc == 0 && z < nz) {
+        const int row = 32 * z + 16 * hh + fr;
+        rsum[row] = (a + a1) + (a2 + a3);
+        rsq[row] = (b + b1) + (b2 + b3);
+      }
+    }
+  }
+  __syncthreads();
+  const int n = cb * 16 + fr;
+  if (blockIdx.x * 4 + wave >= n_cb || n >= p.N) return;
+  const float cs = p.ln_colsum[n], bn = p.bias ? p.bias[n] : 0.f;
+  const float inv = 1.f / (float)p.K;
+#pragma unroll
+  for (int z = 0; z < LMR_NZ; ++z) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 32 * z + 16 * hh + 4 * fc + r;
+        if (z < nz && m < M) {
+          const float mean = rsum[m] * inv;
+          const float rstd = rsqrtf(fmaxf(rsq[m] * inv - mean * mean, 0.f) + p.ln_eps);
+          const float v = hh ? acc1[z][r] : acc0[z][r];
+          reinterpret_cast<float*>(p.C)[(int64_t)m * p.ldc + n] = rstd * (v - mean * cs) + bn;
+        }
+      }
+  }
+}
+
 // LM head (proj_out with the final LayerNorm folded, modeling_whisper.py:790,1080) as a persistent
 // weight stream: the generic kernel above re-reads the 32 activation rows from L2 in every one of its
 // 1,621 workgroups (as many L2 bytes as weight bytes) and runs 1.6 rounds of them.  Here each of
@@ -778,10 +927,37 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
       return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: needs a zero-filled workspace of kw_dec_linear_workspace_bytes()");
   }
   hipStream_t s = (hipStream_t)stream;
-  // LM head: LayerNorm-fused, f32 logits, a wide N and a short K -> the persistent weight stream
-  // (more rows than one chunk: the weight-stationary rows kernel instead, which streams the weights once)
-  const bool lmh = a->ln && a->epilogue == KW_EPI_STORE && a->c_dtype == KW_DT_F32 && a->N >= 8192 &&
-                   (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && !a->gelu && a->scale_cols == 0 && a->M <= KW_LMH_MAX_ROWS;
+  // LM head: LayerNorm-fused, f32 logits, a wide N and a short K -> the persistent weight stream up to
+  // 32 rows, the all-rows GEMM up to LMR_MAXROWS (beam rows), the weight-stationary rows kernel beyond
+  const bool lm_shape = a->ln && a->epilogue == KW_EPI_STORE && a->c_dtype == KW_DT_F32 && a->N >= 8192 && !a->gelu &&
+                        a->scale_cols == 0;
+  if (lm_shape && a->M > KW_LMH_MAX_ROWS && a->M <= LMR_MAXROWS && nkt % 8 == 0) {
+    DecP p{};
+    p.x = reinterpret_cast<const bf16_t*>(a->x);
+    p.ldx = a->ldx;
+    p.ln = 1;
+    p.ln_eps = a->ln_eps;
+    p.ln_colsum = a->ln_colsum;
+    p.W = reinterpret_cast<const bf16x8*>(a->W);
+    p.bias = a->bias;
+    p.C = a->C;
+    p.ldc = a->ldc;
+    p.M = (int)a->M;
+    p.N = (int)a->N;
+    p.K = (int)a->K;
+    const int n_cb = (int)((a->N + 15) / 16);
+    const dim3 grid((unsigned)((n_cb + 3) / 4));
+    switch ((a->M + 63) / 64) {
+      case 1: hipLaunchKernelGGL(lm_head_rows_kernel<1>, grid, dim3(256), 0, s, p); break;
+      case 2: hipLaunchKernelGGL(lm_head_rows_kernel<2>, grid, dim3(256), 0, s, p); break;
+      case 3: hipLaunchKernelGGL(lm_head_rows_kernel<3>, grid, dim3(256), 0, s, p); break;
+      case 4: hipLaunchKernelGGL(lm_head_rows_kernel<4>, grid, dim3(256), 0, s, p); break;
+      default: hipLaunchKernelGGL(lm_head_rows_kernel<5>, grid, dim3(256), 0, s, p); break;
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? KW_OK : kw_set_error(e);
+  }
+  const bool lmh = lm_shape && (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && a->M <= KW_LMH_MAX_ROWS;
   // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each)
   const int64_t step = (g.ks == 1 || lmh) ? a->M : 32 * ZMAX;
   for (int64_t m0 = 0; m0 < a->M; m0 += step) {

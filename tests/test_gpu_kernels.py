@@ -504,7 +504,7 @@ def test_greedy_step_split_rows(rt, n_hist, B, V):
     assert (a_cur, a_nun, a_cnt) == (b_cur, b_nun, b_cnt) and (a_unf == b_unf).all()
 
 
-@pytest.mark.parametrize("M", [32, 5, 70])
+@pytest.mark.parametrize("M", [32, 5, 70, 320, 333])
 @pytest.mark.parametrize("N,K", [(3840, 1280), (51866, 1280), (1152, 384)])
 def test_dec_linear_layernorm(M, N, K):
     """LayerNorm-fused STORE: gamma/beta folded into W and bias as the engine loads them, the rows'
