@@ -199,7 +199,7 @@ def main():
                    "max_length": a.max_length, "new_tokens": new_tokens, "seq_len": 1500,
                    "pipelined": a.pipeline, "encoder_cus": a.encoder_cus if a.pipeline else None,
                    "parallelism": f"dp{world}"},
-        "roofline": {"kernel": "cross_attn_partial (decoder cross-attention K/V stream, per layer)",
+        "roofline": {"kernel": "cross_attn_kernel (decoder cross-attention K/V stream, one launch per layer; rocprof name)",
                      "bound": "hbm", "achieved": cross_bytes / cross_t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": cross_bytes / cross_t / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_launch": cross_bytes, "avg_launch_us": cross_t * 1e6},
