@@ -22,6 +22,7 @@
 //    (W' = W diag(gamma), b' = b + W beta) and colsum(W') is precomputed per column;
 //  * RESID epilogue: h(f32) += acc + bias, plus the bf16 mirror hb = h (the next LayerNorm's operand).
 // Everything is bitwise deterministic: no float atomics, every reduction in a fixed order.
+#include <stdio.h>
 #include <stdlib.h>
 
 #include <algorithm>
@@ -825,9 +826,20 @@ Geo choose(int64_t N, int64_t K) {
   Geo g;
   g.ncb = blocks >= 320 ? 2 : 1;  // wide matrices: reuse each activation fragment twice
   g.ks = 1;
-  if (blocks < 128 && nkt > 80) g.ks = (nkt + 19) / 20;  // few columns, long K: split over workgroups
+  // few columns, long K: split over workgroups, <= 27 k-tiles each (fc2 at large-v3: 6 splits; measured
+  // 10.7 us vs 11.2 us for 8 splits and 13.0 us for 7 -- profiles/r01g_splitk_sweep.txt)
+  if (blocks < 128 && nkt > 80) g.ks = (nkt + 26) / 27;
+  // lab override of the split-K geometry (tools/kbench.py sweeps): KW_DECLIN_SPLITK="ks,ktm"
+  static int lab_ks = -1, lab_ktm = 0;
+  if (lab_ks < 0) {
+    lab_ks = 0;
+    if (const char* e = getenv("KW_DECLIN_SPLITK")) sscanf(e, "%d,%d", &lab_ks, &lab_ktm);
+  }
+  const bool lab = g.ks > 1 && lab_ks >= 1 && lab_ks <= KSMAX;
+  if (lab) g.ks = lab_ks;
   const int per_wg = (nkt + g.ks - 1) / g.ks;
   g.ktm = (g.ncb == 1 && blocks >= 160 && per_wg <= 40) ? 5 : 10;
+  if (lab && (lab_ktm == 5 || lab_ktm == 10)) g.ktm = lab_ktm;
   g.nw = (per_wg + g.ktm - 1) / g.ktm;
   if (g.nw > MAXW) {  // very long K: more splits
     g.nw = MAXW;
