@@ -829,17 +829,24 @@ Geo choose(int64_t N, int64_t K) {
   // few columns, long K: split over workgroups, <= 27 k-tiles each (fc2 at large-v3: 6 splits; measured
   // 10.7 us vs 11.2 us for 8 splits and 13.0 us for 7 -- profiles/r01g_splitk_sweep.txt)
   if (blocks < 128 && nkt > 80) g.ks = (nkt + 26) / 27;
-  // lab override of the split-K geometry (tools/kbench.py sweeps): KW_DECLIN_SPLITK="ks,ktm"
-  static int lab_ks = -1, lab_ktm = 0;
-  if (lab_ks < 0) {
-    lab_ks = 0;
-    if (const char* e = getenv("KW_DECLIN_SPLITK")) sscanf(e, "%d,%d", &lab_ks, &lab_ktm);
+  const int per_wg0 = (nkt + g.ks - 1) / g.ks;
+  // K <= 1280 without a split: 5 k-tiles per wave, up to 8 waves (more loads in flight per workgroup):
+  // 1280x1280 5.8 -> 5.1 us, fc1 9.0 -> 8.6 us (profiles/r01h_declin_geo_sweep.txt); the LM head and
+  // the split fc2 (6 x 27 k-tiles over 3 waves, r01g_splitk_sweep.txt) keep 10
+  g.ktm = (g.ks == 1 && per_wg0 <= 40 && N < 8192) ? 5 : 10;
+  // lab override for one matrix shape (tools/lab/*_sweep.sh): KW_DECLIN_GEO="N,K,ncb,ktm,ks"
+  static int lab[5] = {-1, 0, 0, 0, 0};
+  if (lab[0] < 0) {
+    lab[0] = 0;
+    if (const char* e = getenv("KW_DECLIN_GEO")) sscanf(e, "%d,%d,%d,%d,%d", &lab[0], &lab[1], &lab[2], &lab[3], &lab[4]);
   }
-  const bool lab = g.ks > 1 && lab_ks >= 1 && lab_ks <= KSMAX;
-  if (lab) g.ks = lab_ks;
+  if (lab[0] == N && lab[1] == K && (lab[2] == 1 || lab[2] == 2) && (lab[3] == 5 || lab[3] == 10) && lab[4] >= 1 &&
+      lab[4] <= KSMAX) {
+    g.ncb = lab[2];
+    g.ktm = lab[3];
+    g.ks = lab[4];
+  }
   const int per_wg = (nkt + g.ks - 1) / g.ks;
-  g.ktm = (g.ncb == 1 && blocks >= 160 && per_wg <= 40) ? 5 : 10;
-  if (lab && (lab_ktm == 5 || lab_ktm == 10)) g.ktm = lab_ktm;
   g.nw = (per_wg + g.ktm - 1) / g.ktm;
   if (g.nw > MAXW) {  // very long K: more splits
     g.nw = MAXW;
