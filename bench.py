@@ -33,22 +33,56 @@ BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA spec
 ENC_FLOP_PER_CLIP = 2.2738e12
 
 
+def kernel_source_hash() -> str:
+    """sha256 over the kernel sources (csrc/*.hip, *.h, include/kwhisper.h): identifies the kernels a PMC pass
+    measured (tools/profile.sh stores it beside the counters)."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "kotoba-whisper_amd", "csrc", "*.hip")) +
+                   glob.glob(os.path.join(ROOT, "kotoba-whisper_amd", "csrc", "*.h")) +
+                   [os.path.join(ROOT, "include", "kwhisper.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 FETCH_SIZE summary
-    (profiles/rNN_pmc_fetch.csv, written by tools/profile.sh + tools/rocpd_summary.py): FETCH_SIZE is
+    (profiles/rNN[x]_pmc_fetch.csv, written by tools/profile.sh + tools/rocpd_summary.py): FETCH_SIZE is
     in KB and counts half the bytes of 16-B/lane streaming reads on gfx950 (MI355X_MICROARCH.md
-    section HBM), hence x 1024 x 2.  Returns (bytes, source) or (None, None)."""
+    section HBM), hence x 1024 x 2.  Only a pass over THIS tree's kernels counts: its
+    ``.meta.json`` must carry the current kernel_source_hash(); otherwise traffic is None and the returned
+    note says why.  Returns (bytes or None, note)."""
     import csv
     import glob
+    import re
 
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch.csv")))
+    def order(path):  # r01 < r01j < r02 < r10 (numeric round, then the letter suffix)
+        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+        return (int(m.group(1)), m.group(2)) if m else (-1, "")
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch.csv")), key=order)
     if not files:
-        return None, None
-    with open(files[-1]) as f:
+        return None, "no PMC pass committed"
+    newest = files[-1]
+    rel = os.path.relpath(newest, ROOT)
+    meta = newest[: -len(".csv")] + ".meta.json"
+    try:
+        with open(meta) as f:
+            src = json.load(f).get("kernel_source_sha256")
+    except (OSError, ValueError):
+        src = None
+    if src != kernel_source_hash():
+        return None, f"{rel} measured other kernel sources (stale, not reported)"
+    with open(newest) as f:
         for row in csv.DictReader(f):
             if row["Counter"] == "FETCH_SIZE" and kernel in row["Name"]:
-                return float(row["Mean"]) * 1024 * 2, os.path.relpath(files[-1], ROOT) + " (FETCH_SIZE KB x1024 x2)"
-    return None, None
+                return float(row["Mean"]) * 1024 * 2, rel + " (FETCH_SIZE KB x1024 x2, same kernel sources)"
+    return None, f"{rel} has no {kernel} row"
 
 
 def parse():
@@ -142,7 +176,9 @@ def main():
     if world > 1:
         L = torch.tensor([ids.shape[-1]], device=dev)
         dist.all_reduce(L, op=dist.ReduceOp.MAX)
-        pad = torch.full((*ids.shape[:-1], int(L.item())), 50256, dtype=torch.int32, device=dev)
+        # padded with the tokenizer's pad id, <|endoftext|> (run_pseudo_labelling.py:339)
+        pad = torch.full((*ids.shape[:-1], int(L.item())), model.generation_config.eos_token_id, dtype=torch.int32,
+                         device=dev)
         pad[..., : ids.shape[-1]] = ids
         gathered = [torch.empty_like(pad) for _ in range(world)]
         dist.all_gather(gathered, pad)
@@ -216,8 +252,12 @@ def main():
         cb = hf_cpu_generate_rate(shape, a.cpu_batch, a.max_length)
         result["cpu_baseline"] = {
             "value": cb["audio_seconds_per_second"], "unit": "audio-s/s", "cores": cb["threads"], "kind": "reference",
-            "sample": f"transformers 5.15.0 WhisperForConditionalGeneration.generate fp32 on CPU, {a.cpu_batch} "
-                      f"clips x 30 s, greedy, {cb['new_tokens']} new tokens, {cb['seconds']:.1f} s"}
+            "threads": cb["threads"], "nproc": cb["nproc"], "affinity_cpus": cb["affinity_cpus"],
+            "sample": f"transformers 5.15.0 WhisperForConditionalGeneration.generate fp32 on CPU, torch "
+                      f"{cb['threads']} intra-op threads (the box shows nproc {cb['nproc']}, {cb['affinity_cpus']} in "
+                      f"this process's affinity), a bounded sample of {a.cpu_batch} clips x 30 s (not the config's 32: "
+                      f"about {cb['seconds'] * 32 / max(1, a.cpu_batch) / 60:.0f} min of CPU at 32 if the rate held), "
+                      f"greedy, {cb['new_tokens']} new tokens, {cb['seconds']:.1f} s; run_speed_eval.py:73-78 timing"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -26,6 +26,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <array>
 
 #include "kw_common.h"
 
@@ -834,18 +835,24 @@ Geo choose(int64_t N, int64_t K) {
   // 1280x1280 5.8 -> 5.1 us, fc1 9.0 -> 8.6 us (profiles/r01h_declin_geo_sweep.txt); the LM head and
   // the split fc2 (6 x 27 k-tiles over 3 waves, r01g_splitk_sweep.txt) keep 10
   g.ktm = (g.ks == 1 && per_wg0 <= 40 && N < 8192) ? 5 : 10;
-  // lab override for one matrix shape (tools/lab/*_sweep.sh): KW_DECLIN_GEO="N,K,ncb,ktm,ks"
-  static int lab[5] = {-1, 0, 0, 0, 0};
-  if (lab[0] < 0) {
-    lab[0] = 0;
-    if (const char* e = getenv("KW_DECLIN_GEO")) sscanf(e, "%d,%d,%d,%d,%d", &lab[0], &lab[1], &lab[2], &lab[3], &lab[4]);
-  }
+#ifdef KW_LAB_OVERRIDES
+  // lab builds only (make EXTRA=-DKW_LAB_OVERRIDES OUT=...; tools/lab/*_sweep.sh): KW_DECLIN_GEO="N,K,ncb,ktm,ks"
+  // overrides one matrix shape's geometry; read once, thread-safe (function-local static)
+  static const std::array<int, 5> lab = [] {
+    std::array<int, 5> v{0, 0, 0, 0, 0};
+    if (const char* e = getenv("KW_DECLIN_GEO")) {
+      sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
+      fprintf(stderr, "kwhisper: lab geometry override KW_DECLIN_GEO=%s\n", e);
+    }
+    return v;
+  }();
   if (lab[0] == N && lab[1] == K && (lab[2] == 1 || lab[2] == 2) && (lab[3] == 5 || lab[3] == 10) && lab[4] >= 1 &&
       lab[4] <= KSMAX) {
     g.ncb = lab[2];
     g.ktm = lab[3];
     g.ks = lab[4];
   }
+#endif
   const int per_wg = (nkt + g.ks - 1) / g.ks;
   g.nw = (per_wg + g.ktm - 1) / g.ktm;
   if (g.nw > MAXW) {  // very long K: more splits

@@ -587,11 +587,15 @@ hipError_t launch256(const GemmP& p, int epi, hipStream_t s) {
 
 // 256x256 ping-pong for the big GEMMs; KW_GEMM_TILE=128 (env) forces the 128x128 kernel (A/B runs).
 bool use256(const kw_gemm_args* a) {
-  static int forced = -1;
-  if (forced < 0) {
+#ifdef KW_LAB_OVERRIDES
+  // lab builds only: KW_GEMM_TILE=128 forces the 128x128 kernel (tools/gemm_bench.py)
+  static const int forced = [] {
     const char* e = getenv("KW_GEMM_TILE");
-    forced = (e && atoi(e) == 128) ? 1 : 0;
-  }
+    return (e && atoi(e) == 128) ? 1 : 0;
+  }();
+#else
+  constexpr int forced = 0;
+#endif
   // vector epilogue: ldc, batch strides, head_dim in whole 16-B pieces, the C base 16-B aligned
   const int vec = (a->c_dtype == KW_DT_F32) ? 4 : 8;  // 16-B pieces: 4 f32 / 8 bf16 columns
   const bool aligned = a->ldc % vec == 0 && a->c_batch_stride % vec == 0 &&

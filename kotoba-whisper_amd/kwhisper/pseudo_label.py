@@ -154,7 +154,7 @@ def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device,
 
 
 def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *, batch_size: int,
-                 gen_kwargs: Optional[dict] = None, pad_token_id: int = 50256, comm_device=None,
+                 pad_token_id: int, gen_kwargs: Optional[dict] = None, comm_device=None,
                  on_step: Optional[Callable[[int, int], None]] = None, legacy_prompt_in_output: bool = False):
     """Transcribe items 0..n_items-1 data-parallel; returns (item_indices, predictions) in dataset order
     on every rank (``run_pseudo_labelling.py:333-344``).
@@ -162,6 +162,10 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
     ``features(indices)`` returns the (b, n_mels, 3000) log-mel batch for those dataset indices (on the
     model's device); ``predictions`` is a list of 1-D int64 numpy arrays, one per item, each padded to
     its gather round's common width exactly as the reference's ``eval_preds`` rows are.
+    ``pad_token_id`` is required and is the TOKENIZER's pad id, as the reference pads across processes with
+    ``tokenizer.pad_token_id`` (run_pseudo_labelling.py:339) -- for the Whisper tokenizers that is
+    ``<|endoftext|>`` (the eos id, 50257), not ``generation_config.pad_token_id`` (50256), which only pads
+    rows inside one generate() output.
     ``legacy_prompt_in_output`` prepends ``legacy_prompt(...)`` to every row (needs ``language``)."""
     gen_kwargs = dict(gen_kwargs or {})
     prompt = None
@@ -180,8 +184,8 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
 
 
 def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *,
-                           batch_size: int, text_lang_task: Sequence[tuple], gen_kwargs: Optional[dict] = None,
-                           pad_token_id: int = 50256, comm_device=None,
+                           batch_size: int, text_lang_task: Sequence[tuple], pad_token_id: int,
+                           gen_kwargs: Optional[dict] = None, comm_device=None,
                            on_step: Optional[Callable[[int, int], None]] = None):
     """``run_pseudo_labelling_v3.py:299-321``: every batch is decoded once per (text, lang, task) triple.
     Returns (item_indices, {text: predictions}) in dataset order; ``whisper_<text>`` is the column the

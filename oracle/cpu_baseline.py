@@ -59,5 +59,9 @@ def hf_cpu_generate_rate(shape, batch: int, max_length: int, threads: int | None
         t0 = time.perf_counter()
         out = m.generate(feats, max_length=max_length, language="ja", task="transcribe")
         dt = time.perf_counter() - t0
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {"seconds": dt, "batch": batch, "new_tokens": int(out.shape[1]), "threads": threads,
-            "audio_seconds_per_second": batch * 30.0 / dt}
+            "nproc": os.cpu_count(), "affinity_cpus": affinity, "audio_seconds_per_second": batch * 30.0 / dt}

@@ -81,3 +81,27 @@ def log_mel(audio_batch: np.ndarray, n_mels: int) -> np.ndarray:
         lg = np.maximum(lg, lg.max() - np.float32(8.0))
         out[i] = (lg + np.float32(4.0)) / np.float32(4.0)
     return out
+
+
+def log_mel_padded(audio_list, n_mels: int, return_attention_mask: bool = True):
+    """``WhisperFeatureExtractor.__call__(raw, padding="longest", truncation=False,
+    return_attention_mask=True)`` (TF/models/whisper/feature_extraction_whisper.py:280-346): every clip is
+    zero-padded to the longest clip of the batch (``SequenceFeatureExtractor.pad``), the log-mel runs over
+    that length (per-clip max clamp over the padded clip), and the sample-level mask is subsampled by the
+    hop (``[:, ::160]``, minus the last entry when the length is not a multiple of 160, :333-340).
+
+    Returns (features (B, n_mels, L // 160) f32, attention_mask (B, L // 160) int32 or None)."""
+    clips = [np.asarray(a, dtype=np.float32).reshape(-1) for a in audio_list]
+    n = max(c.shape[0] for c in clips)
+    batch = np.zeros((len(clips), n), dtype=np.float32)
+    mask = np.zeros((len(clips), n), dtype=np.int32)
+    for i, c in enumerate(clips):
+        batch[i, : c.shape[0]] = c
+        mask[i, : c.shape[0]] = 1
+    feats = log_mel(batch, n_mels)
+    if not return_attention_mask:
+        return feats, None
+    m = mask[:, ::HOP]
+    if n % HOP != 0:
+        m = m[:, :-1]
+    return feats, m

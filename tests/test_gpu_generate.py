@@ -157,7 +157,7 @@ def test_large_bf16_vs_reference(gold):
     got = torch.gather(lg[:, : idx.shape[1]], -1, torch.from_numpy(idx.astype(np.int64))).numpy()
     err = np.abs(got - val)
     print("large-v3 bf16 teacher-forced logit err: max %.4f mean %.4f" % (err.max(), err.mean()))
-    assert err.mean() < 0.1
+    assert err.max() < 0.35 and err.mean() < 0.03  # the same bars as config 3 at B = 32 (test_gpu_workloads.py)
     del model, sess
     torch.cuda.empty_cache()
 
@@ -195,48 +195,6 @@ def test_generate_multitask_reuses_encoder(gold, tiny32, ts):
 
 
 @pytest.mark.parametrize("ts", [False, True])
-def test_asr_pipeline_chunked(tiny32, ts):
-    """ASRPipeline (chunk_length_s=15, batch_size=3, two clips of 40 s and 7 s) equals the
-    reference composition chunk by chunk: transformers' chunk_iter windows -> generate() one window at a
-    time -> transformers' own _decode_asr merge (stub tokenizer, see test_pipeline.py)."""
-    from transformers.models.whisper.tokenization_whisper import _decode_asr
-    from transformers.pipelines.automatic_speech_recognition import chunk_iter as hf_chunk_iter
-
-    from kwhisper.feature_extraction import WhisperFeatureExtractor
-    from kwhisper.pipeline import ASRPipeline
-    from kwhisper.synthetic import dummy_audio
-    from test_pipeline import StubTokenizer
-
-    tk = StubTokenizer()
-    tk.all_special_ids = tk.all_special_ids + [tiny32.generation_config.pad_token_id]
-    long = np.concatenate([dummy_audio(i) for i in range(2)])[: 16000 * 40].astype(np.float32)
-    clips = [long, long[: 16000 * 7]]
-    gk = dict(language="ja", task="transcribe", max_length=40)
-    pipe = ASRPipeline(tiny32, tokenizer=tk, chunk_length_s=15, batch_size=3, generate_kwargs=gk)
-    got = pipe([{"array": c, "sampling_rate": 16000, "path": f"c{i}"} for i, c in enumerate(clips)],
-               return_timestamps=ts)
-    fe = WhisperFeatureExtractor(feature_size=TINY.num_mel_bins)
-
-    class _FE:
-        sampling_rate = 16000
-
-        def __call__(self, chunk, **kw):
-            return {"chunk": chunk}
-
-    for clip, res in zip(clips, got):
-        outputs = []
-        for item in hf_chunk_iter(clip, _FE(), 240000, 40000, 40000):
-            feats = fe(item["chunk"])["input_features"]
-            ids = tiny32.generate(feats, return_timestamps=ts, **gk).cpu()
-            n, left, right = item["stride"]
-            outputs.append({"tokens": ids, "stride": (n / 16000, left / 16000, right / 16000)})
-        text, optional = _decode_asr(tk, outputs, return_timestamps=ts, return_language=None, time_precision=0.02)
-        assert res["text"] == text and len(text) > 0
-        assert res.get("chunks") == optional.get("chunks")
-        assert "path" not in res  # a datasets audio dict's path is dropped (automatic_speech_recognition.py:391-393)
-
-
-@pytest.mark.parametrize("ts", [False, True])
 def test_generate_pipelined_matches_per_batch(gold, tiny32, ts):
     """generate_pipelined (next batch's log-mel + encoder + cross-K/V on a CU-restricted stream beside this
     batch's decode) yields exactly generate() per batch; with timestamps it runs batch by batch."""
@@ -265,7 +223,7 @@ def test_tiny_fp32_longform_bitexact(gold, tiny32):
     from _util import longform_inputs, segments_of
 
     g = gold("tiny_longform_fp32")
-    feats, mask, one = longform_inputs(g["clips"])
+    feats, mask, one = longform_inputs(g["clips"])  # oracle log-mel (same tokens as HF's features)
     res = tiny32.generate(torch.from_numpy(feats).cuda(), attention_mask=torch.from_numpy(mask).cuda(),
                           language="ja", task="transcribe", return_timestamps=True, return_segments=True)
     np.testing.assert_array_equal(res["sequences"].cpu().numpy(), g["long_ts_segments_tokens"])
@@ -279,44 +237,3 @@ def test_tiny_fp32_longform_bitexact(gold, tiny32):
     np.testing.assert_array_equal(plain.cpu().numpy(), g["long_ts_tokens"])
     single = tiny32.generate(torch.from_numpy(one).cuda(), language="ja", task="transcribe", return_timestamps=True)
     np.testing.assert_array_equal(single.cpu().numpy(), g["long_single_tokens"])
-
-
-def test_asr_pipeline_unchunked_longform(gold, tiny32):
-    """ASRPipeline without chunk_length_s on > 30 s clips: each item is one long-form generate (the seek
-    loop), batched with the reference's collate (features padded, attention masks); == transformers'
-    _decode_asr over the HF long-form token rows of the same clips (fixture tiny_longform_fp32).
-    The feature extractor is transformers' own here, so the comparison is exact (ours is tested apart)."""
-    from transformers import WhisperFeatureExtractor as HFFE
-    from transformers.models.whisper.tokenization_whisper import _decode_asr
-
-    from _util import long_audio
-    from kwhisper.pipeline import ASRPipeline
-    from test_pipeline import StubTokenizer
-
-    class _FE:
-        sampling_rate, n_samples, padding_value, chunk_length = 16000, 480000, 0.0, 30
-        device = torch.device("cuda")
-
-        def __init__(self):
-            self.fe = HFFE(feature_size=TINY.num_mel_bins)
-
-        def __call__(self, audio, **kw):
-            kw.pop("device", None)
-            out = self.fe(audio, return_tensors="pt", **kw)
-            return {k: v.cuda() for k, v in out.items()}
-
-    g = gold("tiny_longform_fp32")
-    clips = []
-    for c in g["clips"]:
-        kind, seed, sec = str(c).split(":")
-        clips.append(long_audio(kind, int(seed), float(sec)))
-    tk = StubTokenizer()
-    tk.all_special_ids = tk.all_special_ids + [tiny32.generation_config.pad_token_id]
-    pipe = ASRPipeline(tiny32, feature_extractor=_FE(), tokenizer=tk, batch_size=3,
-                       generate_kwargs=dict(language="ja", task="transcribe"))
-    got = pipe([{"array": c, "sampling_rate": 16000} for c in clips], return_timestamps=True)
-    for i, res in enumerate(got):
-        text, optional = _decode_asr(tk, [{"tokens": torch.from_numpy(g["long_ts_tokens"][i: i + 1])}],
-                                     return_timestamps=True, return_language=None, time_precision=0.02)
-        assert res["text"] == text and len(text) > 0
-        assert res["chunks"] == optional["chunks"]

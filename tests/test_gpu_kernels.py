@@ -504,8 +504,8 @@ def test_greedy_step_split_rows(rt, n_hist, B, V):
     assert (a_cur, a_nun, a_cnt) == (b_cur, b_nun, b_cnt) and (a_unf == b_unf).all()
 
 
-@pytest.mark.parametrize("M", [32, 5, 70, 320, 333])
-@pytest.mark.parametrize("N,K", [(3840, 1280), (51866, 1280), (1152, 384)])
+@pytest.mark.parametrize("M", [32, 5, 1, 70, 320, 333])
+@pytest.mark.parametrize("N,K", [(3840, 1280), (5120, 1280), (1280, 1280), (51866, 1280), (1152, 384)])
 def test_dec_linear_layernorm(M, N, K):
     """LayerNorm-fused STORE: gamma/beta folded into W and bias as the engine loads them, the rows'
     statistics computed in-kernel from the bf16 operand; against an fp32 reference of LN(x) W^T + b."""
@@ -521,6 +521,29 @@ def test_dec_linear_layernorm(M, N, K):
                       C=C)()
     xn = torch.nn.functional.layer_norm(hb.float(), (K,), g, bb, 1e-5).bfloat16()
     torch.testing.assert_close(C, _ref_gemm(xn, W, bias), atol=4e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("M", [1, 5, 32])
+def test_dec_linear_ln_gelu_bf16(M):
+    """The production fc1 variant: N 5120, K 1280, LayerNorm fused, exact-erf GELU, bf16 STORE,
+    at decode row counts (<KTM=5, NCB=2, LNA> geometry), against fp32 GELU(LN(x) W^T + b)."""
+    torch.manual_seed(M)
+    N, K = 5120, 1280
+    h = torch.randn(M, K, device="cuda") * 2 + 0.5
+    hb = h.bfloat16()
+    g = 1 + 0.1 * torch.randn(K, device="cuda")
+    bb = 0.1 * torch.randn(K, device="cuda")
+    W = (torch.randn(N, K, device="cuda") / K ** 0.5).bfloat16()
+    bias = 0.1 * torch.randn(N, device="cuda")
+    Wf = (W.float() * g[None, :]).bfloat16()
+    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    ops.DecLinearPlan(hb, ops.pack_weight(Wf), M, N, K, ln=(1e-5, ops.ln_colsum(Wf)), bias=bias + W.float() @ bb,
+                      C=C, gelu=True)()
+    xn = torch.nn.functional.layer_norm(hb.float(), (K,), g, bb, 1e-5).bfloat16()
+    ref = torch.nn.functional.gelu(_ref_gemm(xn, W, bias))
+    err = (C.float() - ref).abs()
+    print(f"fc1 LN+GELU bf16 M={M}: max err {err.max().item():.4f}")
+    torch.testing.assert_close(C.float(), ref, atol=5e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("M", [64, 70, 320])

@@ -1,0 +1,366 @@
+"""The BASELINE workloads themselves on the GPU, against fixtures of the reference path.
+
+* config 3 (the bench workload: large-v3, 32 clips, greedy, 128 new tokens, no timestamps;
+  run_pseudo_labelling.py:338): the bf16 production path -- graph-replayed generate(), packed
+  LayerNorm-folded decode linears, LM head kernel -- against transformers' fp32 run of the same 32 clips
+  (tests/golden/large_v3_b32_fp32.npz): margin-gated token equality, teacher-forced max / mean logit error,
+  batch invariance; and the fp32 parity mode bit-exact at the same size.
+* config 5 (kotoba-whisper-v2.0 layout, beam 5 + timestamps, chunked pipeline; run_short_form_eval.py:184-191):
+  fp32 beam search bit-exact, bf16 beam hypotheses rescored by the fp32 engine, and the chunked
+  ASRPipeline against the real transformers pipeline's output.
+* config 4 (run_pseudo_labelling.py:333-344 with timestamps, its default :99-102): pseudo_label() over the
+  engine at W = 1 and W = 2 (two spawned processes on cuda:0 over gloo).
+
+Every measured error is printed (run with -s; the round's pytest log is committed under profiles/).
+"""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from kwhisper.config import KOTOBA_V2, LARGE_V3, TINY, generation_constants  # noqa: E402
+from kwhisper.synthetic import synthetic_state_dict  # noqa: E402
+
+from _util import OracleFeatureExtractor, StubTok, clip_audio, jsonable, oracle_features  # noqa: E402
+
+# bf16 noise floor for greedy tokens: a step whose fp32 top-1/top-2 margin is below this may flip under
+# bf16 arithmetic (the measured teacher-forced logit error at large-v3 is printed by the test below)
+MARGIN_FLOOR = 0.1
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _model(shape, dtype, pad=None):
+    from kwhisper.generation import KWhisperForConditionalGeneration
+
+    return KWhisperForConditionalGeneration.from_state_dict(
+        shape, synthetic_state_dict(shape, 0), dtype=dtype, generation_config=generation_constants(shape, pad))
+
+
+def _free():
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def _gated_equal(toks, want, margin, floor=MARGIN_FLOOR):
+    """Rows equal up to each row's first step whose reference margin is below ``floor``; returns the
+    number of tokens compared."""
+    n = 0
+    for b in range(want.shape[0]):
+        unsafe = np.nonzero(margin[b] < floor)[0]
+        upto = int(unsafe[0]) if unsafe.size else want.shape[1]
+        np.testing.assert_array_equal(toks[b, :upto], want[b, :upto], err_msg=f"row {b} (first unsafe step {upto})")
+        n += upto
+    return n
+
+
+# ---------------------------------------------------------------------------------------------------------
+# config 3
+
+
+@pytest.fixture(scope="module")
+def large_b32_gold(gold):
+    g = gold("large_v3_b32_fp32")
+    return g, oracle_features(LARGE_V3, g["cases"])
+
+
+def test_config3_bf16_generate_b32(large_b32_gold):
+    """The measured bf16 path at the bench's exact shape: B = 32, 128 graph-replayed decode steps."""
+    g, feats_np = large_b32_gold
+    model = _model(LARGE_V3, torch.bfloat16)
+    feats = torch.from_numpy(feats_np).cuda()
+    eng = model.engine
+    # encoder (bf16 residual stream, as the reference's bf16 model)
+    enc = eng.encode(feats)
+    e = enc.view(32, 1500, 1280).float().cpu().numpy()[:, ::250, :]
+    ref = g["enc_slice"]
+    rel = np.abs(e - ref).max() / np.abs(ref).max()
+    rel_mean = np.abs(e - ref).mean() / np.abs(ref).mean()
+    print(f"\nconfig3 bf16 encoder: max |err| / max |ref| = {rel:.4f}, mean |err| / mean |ref| = {rel_mean:.4f}")
+    assert rel < 0.05 and rel_mean < 0.01
+    # teacher-forced logits through the production decode kernels (packed weights, folded LayerNorms, LM head)
+    sess = eng.new_session(32, enc)
+    seq = torch.from_numpy(g["greedy_sequences"])
+    lg = sess.teacher_forced_logits(seq[:, :-1], 4)
+    idx = torch.from_numpy(g["greedy_logits_top_idx"].astype(np.int64)).cuda()
+    got = torch.gather(lg[:, : idx.shape[1]], -1, idx).cpu().numpy()
+    err = np.abs(got - g["greedy_logits_top_val"])
+    top1 = lg[:, : idx.shape[1]].argmax(-1).cpu().numpy()
+    agree = (top1 == g["greedy_logits_top_idx"][..., 0]).mean()
+    print(f"config3 bf16 teacher-forced top-8 logit err over {err.size} values: max {err.max():.4f} "
+          f"mean {err.mean():.5f} p99 {np.percentile(err, 99):.4f}; top-1 agreement {agree:.4f}")
+    assert err.max() < 0.35 and err.mean() < 0.03
+    del lg, sess
+    _free()
+    # the graph-replayed generate() (what bench.py times)
+    toks = model.generate(feats, language="ja", task="transcribe", max_length=128).cpu().numpy()
+    want = g["greedy_tokens"]
+    assert toks.shape == want.shape
+    n = _gated_equal(toks, want, g["greedy_margin"])
+    full = int((toks == want).all(1).sum())
+    print(f"config3 bf16 generate: {n} of {want.size} tokens compared (margin >= {MARGIN_FLOOR}), all equal; "
+          f"{full}/32 rows identical end to end; {(toks == want).mean():.4f} of all positions equal")
+    # batch invariance: two of the clips alone give the rows they get inside the batch of 32
+    sub = [0, 17]
+    toks2 = model.generate(feats[sub], language="ja", task="transcribe", max_length=128).cpu().numpy()
+    np.testing.assert_array_equal(toks2, toks[sub])
+    del model
+    _free()
+
+
+def test_config3_fp32_generate_b32_bitexact(large_b32_gold):
+    """North star: greedy token ids bit-exact with the HF fp32 reference, at the config-3 shape (fp32 parity
+    mode: exact-fp32 MFMA GEMMs, separate LayerNorms)."""
+    g, feats_np = large_b32_gold
+    model = _model(LARGE_V3, torch.float32)
+    toks = model.generate(torch.from_numpy(feats_np).cuda(), language="ja", task="transcribe", max_length=128)
+    np.testing.assert_array_equal(toks.cpu().numpy(), g["greedy_tokens"])
+    del model
+    _free()
+
+
+# ---------------------------------------------------------------------------------------------------------
+# config 5
+
+
+@pytest.fixture(scope="module")
+def kotoba32():
+    m = _model(KOTOBA_V2, torch.float32)
+    yield m
+    del m
+    _free()
+
+
+@pytest.mark.parametrize("mode", ["beam5_ts", "beam5"])
+def test_config5_kotoba_fp32_beam_bitexact(gold, kotoba32, mode):
+    g = gold("kotoba_v2_beam_fp32")
+    kw = {"beam5_ts": dict(return_timestamps=True), "beam5": dict(return_timestamps=False)}[mode]
+    feats = torch.from_numpy(oracle_features(KOTOBA_V2, g["cases"])).cuda()
+    toks = kotoba32.generate(feats, language="ja", task="transcribe", num_beams=5, max_length=48, **kw)
+    np.testing.assert_array_equal(toks.cpu().numpy(), g[f"{mode}_tokens"])
+
+
+def _tf_logprobs(eng, enc_row, seq, P):
+    """Per-token log-softmax of the teacher-forced logits of ``seq`` (1-D, prompt + generated) for positions
+    P..len-1 (the generated tokens)."""
+    sess = eng.new_session(1, enc_row)
+    t = torch.as_tensor(seq, dtype=torch.int64)[None]
+    lg = sess.teacher_forced_logits(t, P)[0, : t.shape[1] - P].float()
+    lp = torch.log_softmax(lg, -1)
+    return lp.gather(-1, t[0, P:].cuda()[:, None])[:, 0].double().cpu().numpy()
+
+
+def test_config5_kotoba_bf16_beam_rescored(gold, kotoba32):
+    """bf16 beam search (no timestamps, one seek pass) on the kotoba-v2.0 layout: every item's chosen
+    hypothesis, rescored by the fp32 engine (pinned bit-exact to HF above), is as good as the fp32 beam's
+    choice within the bf16 scoring noise of the two hypotheses (HF beam score: sum of log-probs / length,
+    utils.py:3182)."""
+    g = gold("kotoba_v2_beam_fp32")
+    gen = generation_constants(KOTOBA_V2)
+    feats = torch.from_numpy(oracle_features(KOTOBA_V2, g["cases"])).cuda()
+    m16 = _model(KOTOBA_V2, torch.bfloat16)
+    kw = dict(language="ja", task="transcribe", num_beams=5, max_length=48, return_timestamps=False)
+    t16 = m16.generate(feats, **kw).cpu().numpy()
+    t32 = g["beam5_tokens"]
+    prompt = [gen.decoder_start_token_id, gen.lang_to_id["<|ja|>"], gen.task_to_id["transcribe"],
+              gen.no_timestamps_token_id]
+    P, max_new = len(prompt), 48  # max_length grows by the prompt (generation_whisper.py:1935-1940)
+    e32 = kotoba32.engine.encode(feats).view(4, 1500, -1)
+    e16 = m16.engine.encode(feats).view(4, 1500, -1)
+
+    def hyp(row):
+        r = [int(x) for x in row]
+        while r and r[-1] == gen.pad_token_id:
+            r.pop()
+        return prompt + r + ([gen.eos_token_id] if len(r) < max_new else [])
+
+    same = 0
+    for b in range(4):
+        h16, h32 = hyp(t16[b]), hyp(t32[b])
+        s = {}
+        for name, h in (("h16", h16), ("h32", h32)):
+            lp32 = _tf_logprobs(kotoba32.engine, e32[b:b + 1].reshape(1500, -1), h, P)
+            lp16 = _tf_logprobs(m16.engine, e16[b:b + 1].reshape(1500, -1), h, P)
+            s[name] = (lp32.sum() / len(lp32), lp16.sum() / len(lp16))
+        tol = abs(s["h16"][1] - s["h16"][0]) + abs(s["h32"][1] - s["h32"][0]) + 1e-4
+        same += h16 == h32
+        print(f"\nconfig5 bf16 beam item {b}: same hypothesis {h16 == h32}; fp32 score of bf16 choice "
+              f"{s['h16'][0]:.5f} vs fp32 choice {s['h32'][0]:.5f} (tolerance {tol:.5f})")
+        assert s["h16"][0] >= s["h32"][0] - tol
+    print(f"config5 bf16 beam: {same}/4 items chose the fp32 hypothesis")
+    del m16
+    _free()
+
+
+@pytest.mark.parametrize("fe_kind", ["oracle", "hip"])
+def test_config5_pipeline_kotoba_fp32(gold, kotoba32, fe_kind):
+    """run_short_form_eval.py:184-191 at config 5: ASRPipeline(chunk_length_s=15, batch_size=4, beam 5,
+    timestamps) == the real transformers pipeline (tests/golden/pipeline_kotoba_v2_fp32.npz), window batch by
+    window batch and in the merged text / chunks.  ``fe_kind``: the oracle log-mel (exact inputs) or the
+    product HIP log-mel."""
+    from kwhisper.pipeline import ASRPipeline
+
+    g = gold("pipeline_kotoba_v2_fp32")
+    _check_pipeline(g, kotoba32, KOTOBA_V2, fe_kind)
+
+
+def _check_pipeline(g, model, shape, fe_kind, batch_size=None, ts_keys=None):
+    from kwhisper.pipeline import ASRPipeline
+
+    gk = json.loads(str(g["generate_kwargs"]))
+    fe = OracleFeatureExtractor(shape.num_mel_bins) if fe_kind == "oracle" else None
+    pipe = ASRPipeline(model, feature_extractor=fe, tokenizer=StubTok(generation_constants(shape)),
+                       chunk_length_s=float(g["chunk_length_s"]), batch_size=batch_size or int(g["batch_size"]),
+                       generate_kwargs=gk)
+    calls = []
+    orig = model.generate
+
+    def rec(*a, **kw):
+        out = orig(*a, **kw)
+        calls.append((out["sequences"] if isinstance(out, dict) else out).cpu().numpy())
+        return out
+
+    model.generate = rec
+    try:
+        for key in ts_keys or [k[:-7] for k in g if k.endswith("_result")]:
+            ts = key == "ts1"
+            calls.clear()
+            got = pipe([{"array": clip_audio(c), "sampling_rate": 16000} for c in g["clips"]], return_timestamps=ts)
+            if batch_size is None:  # the reference's window batches, one by one
+                assert len(calls) == int(g[f"{key}_n_calls"])
+                for i, c in enumerate(calls):
+                    np.testing.assert_array_equal(c, g[f"{key}_call{i}"], err_msg=f"{key} window batch {i}")
+            assert jsonable(got) == json.loads(str(g[f"{key}_result"]))
+    finally:
+        del model.generate
+
+
+def test_config5_pipeline_kotoba_bf16_runs(gold):
+    """The same pipeline on the bf16 engine (the measured configuration): runs end to end over device beam
+    search; its agreement with the fp32 reference text is printed, not gated (beam hypotheses are not
+    margin-gateable token by token; test_config5_kotoba_bf16_beam_rescored bounds their quality)."""
+    from kwhisper.pipeline import ASRPipeline
+
+    g = gold("pipeline_kotoba_v2_fp32")
+    m16 = _model(KOTOBA_V2, torch.bfloat16)
+    gk = json.loads(str(g["generate_kwargs"]))
+    pipe = ASRPipeline(m16, tokenizer=StubTok(generation_constants(KOTOBA_V2)), chunk_length_s=15,
+                       batch_size=int(g["batch_size"]), generate_kwargs=gk)
+    got = pipe([{"array": clip_audio(c), "sampling_rate": 16000} for c in g["clips"]], return_timestamps=True)
+    want = json.loads(str(g["ts1_result"]))
+    for i, (a, b) in enumerate(zip(jsonable(got), want)):
+        ta, tb = a["text"], b["text"]
+        k = next((j for j in range(min(len(ta), len(tb))) if ta[j] != tb[j]), min(len(ta), len(tb)))
+        print(f"\nconfig5 bf16 pipeline clip {i}: text identical {ta == tb}; common prefix {k} of {len(tb)} chars; "
+              f"{len(a['chunks'])} vs {len(b['chunks'])} chunks")
+        assert len(ta) > 0 and all(set(c) == {"timestamp", "text"} for c in a["chunks"])
+    del m16
+    _free()
+
+
+# ---------------------------------------------------------------------------------------------------------
+# tiny pipeline fixtures (the reference's own pipeline; no transformers on the GPU box)
+
+
+@pytest.fixture(scope="module")
+def tiny32():
+    m = _model(TINY, torch.float32)
+    yield m
+    del m
+
+
+@pytest.mark.parametrize("fe_kind", ["oracle", "hip"])
+def test_pipeline_chunked_tiny_vs_reference(gold, tiny32, fe_kind):
+    """ASRPipeline(chunk_length_s=15, batch_size=3) on a 40 s and a 7 s clip, with and without timestamps,
+    == transformers' pipeline (tests/golden/pipeline_tiny_fp32.npz)."""
+    _check_pipeline(gold("pipeline_tiny_fp32"), tiny32, TINY, fe_kind)
+
+
+@pytest.mark.parametrize("bs", [1, 3])
+def test_pipeline_longform_tiny_vs_reference(gold, tiny32, bs):
+    """ASRPipeline without chunking on 45 / 70 / 12 s clips: each item one long-form generate (the seek
+    loop) == transformers' pipeline at batch_size 1 (tests/golden/pipeline_tiny_longform_fp32.npz; at
+    batch_size > 1 transformers 5.15 cannot collate long-form items of different lengths, so batch 3 is
+    held to the same output)."""
+    _check_pipeline(gold("pipeline_tiny_longform_fp32"), tiny32, TINY, "oracle", batch_size=None if bs == 1 else bs)
+
+
+# ---------------------------------------------------------------------------------------------------------
+# config 4: the pseudo-labelling loop over the engine
+
+N_ITEMS, BS = 10, 4
+GEN_KW = dict(language="ja", task="transcribe", return_timestamps=True, max_length=64)
+
+
+def _items():
+    """Items 0-3 are the tiny fixture clips (so batch 0 is pinned to the HF tokens), the rest other clips."""
+    return ["dummy:0", "dummy:1", "tone:0", "tone:1"] + [f"dummy:{10 + i}" for i in range(N_ITEMS - 4)]
+
+
+def _item_features(idx):
+    return torch.from_numpy(oracle_features(TINY, [_items()[i] for i in idx])).cuda()
+
+
+def _pad_to(rows, width, pad):
+    out = np.full((len(rows), width), pad, dtype=np.int64)
+    for i, r in enumerate(rows):
+        out[i, : len(r)] = r
+    return out
+
+
+def _pl_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    from kwhisper.pseudo_label import pseudo_label
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        model = _model(TINY, torch.float32)
+        pad = model.generation_config.eos_token_id  # the tokenizer's pad id (<|endoftext|>), run_pseudo_labelling.py:339
+        ids, preds = pseudo_label(model, _item_features, N_ITEMS, batch_size=BS, gen_kwargs=GEN_KW,
+                                  pad_token_id=pad, comm_device="cpu")
+        w = max(len(p) for p in preds)
+        np.savez(os.path.join(out_dir, f"r{rank}.npz"), ids=np.array(ids), preds=_pad_to(preds, w, pad))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config4_pseudo_label_engine(gold, tiny32, tmp_path):
+    """run_pseudo_labelling.py:333-344 over the HIP engine with timestamps: W = 1 equals per-batch generate()
+    (batch 0 = the HF fixture's greedy_ts tokens); W = 2 (two processes on this GPU, gloo) gathers the same
+    predictions in dataset order."""
+    import torch.multiprocessing as mp
+
+    from kwhisper.pseudo_label import pseudo_label
+
+    g = gold("tiny_fp32")
+    pad = tiny32.generation_config.eos_token_id
+    ids1, preds1 = pseudo_label(tiny32, _item_features, N_ITEMS, batch_size=BS, gen_kwargs=GEN_KW, pad_token_id=pad)
+    assert ids1 == list(range(N_ITEMS))
+    for b0 in range(0, N_ITEMS, BS):
+        idx = list(range(b0, min(N_ITEMS, b0 + BS)))
+        want = tiny32.generate(_item_features(idx), **GEN_KW).cpu().numpy()
+        got = np.stack([preds1[i] for i in idx])
+        np.testing.assert_array_equal(got, want)
+    fx = tiny32.generate(_item_features(range(4)), language="ja", task="transcribe", return_timestamps=True).cpu().numpy()
+    np.testing.assert_array_equal(fx, g["greedy_ts_tokens"])  # the loop's inputs are the pinned clips
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_pl_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    w = max(len(p) for p in preds1)
+    for r in range(2):
+        z = np.load(tmp_path / f"r{r}.npz")
+        assert z["ids"].tolist() == list(range(N_ITEMS))
+        width = max(w, z["preds"].shape[1])
+        np.testing.assert_array_equal(_pad_to(list(z["preds"]), width, pad), _pad_to(preds1, width, pad))
+    print(f"\nconfig4 pseudo_label: W=1 and W=2 (gloo, 2 processes on cuda:0) agree on {N_ITEMS} items")

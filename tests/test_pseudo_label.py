@@ -196,7 +196,14 @@ def test_legacy_prompt_in_output(ts):
         assert b[: len(pre)].tolist() == pre
         np.testing.assert_array_equal(b[len(pre):], a)
     with pytest.raises(ValueError):
-        pseudo_label(M(), _features, 2, batch_size=4, legacy_prompt_in_output=True, gen_kwargs={})
+        pseudo_label(M(), _features, 2, batch_size=4, pad_token_id=PAD, legacy_prompt_in_output=True, gen_kwargs={})
+
+
+def test_pad_token_id_is_required():
+    """The cross-process pad is the tokenizer's pad id (run_pseudo_labelling.py:339), which the caller must
+    state: no default that could silently be generation_config.pad_token_id."""
+    with pytest.raises(TypeError):
+        pseudo_label(_StubModel(), _features, 3, batch_size=4)
 
 
 def test_transcription_arrow_column_matches_datasets(tmp_path):

@@ -85,7 +85,7 @@ def config4(a, world, rank, dev):
         dist.barrier()
     t0 = time.perf_counter()
     ids, preds = pseudo_label(model, features, n, batch_size=a.batch, gen_kwargs=gen_kw,
-                              pad_token_id=model.generation_config.pad_token_id)
+                              pad_token_id=model.generation_config.eos_token_id)  # tokenizer pad = <|endoftext|>
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

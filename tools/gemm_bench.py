@@ -1,7 +1,7 @@
 #!/usr/bin/env python
 """Encoder GEMM microbenchmark (development tool): TFLOP/s of kw_gemm at large-v3 B=32 shapes.
 
-    KW_GEMM_TILE=128 python tools/gemm_bench.py   # 128x128 kernel
+    KW_GEMM_TILE=128 KWHISPER_LIB=<lab build, -DKW_LAB_OVERRIDES> python tools/gemm_bench.py   # 128x128 kernel
     python tools/gemm_bench.py                    # default (256x256 ping-pong where it applies)
 """
 from __future__ import annotations

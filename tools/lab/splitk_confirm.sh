@@ -1,6 +1,9 @@
 #!/bin/bash
 # A/B of the fc2 split-K geometry: kernel alone (alternating) and the whole bench.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
+# the override is compiled into lab builds only:
+#   make -C kotoba-whisper_amd/csrc EXTRA=-DKW_LAB_OVERRIDES BUILD=build_lab OUT=../kwhisper/libkwhisper_lab.so
+export KWHISPER_LIB="${KWHISPER_LIB:-$PWD/kotoba-whisper_amd/kwhisper/libkwhisper_lab.so}"
 mkdir -p gpurun_out
 for rep in 1 2 3; do
   for cfg in default 10,6 10,7; do

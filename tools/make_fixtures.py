@@ -217,6 +217,157 @@ def longform_fixtures():
     print(f"tiny_longform fixtures done in {time.time() - t0:.1f}s")
 
 
+# ---------------------------------------------------------------------------------------------------------------
+# Round 2: the measured workloads themselves (BASELINE configs 3 and 5)
+
+B32_CASES = [("dummy", s) for s in range(16)] + [("tone", s) for s in range(16)]
+
+
+def large_b32_fixtures():
+    """tests/golden/large_v3_b32_fp32.npz: BASELINE config 3 itself -- large-v3, 32 clips, greedy,
+    ``max_length=128`` (128 new tokens), no timestamps (run_pseudo_labelling.py:338 with the bench's
+    gen_kwargs).  Stores the plain token matrix, per-step top-2 margins of the processed scores and the
+    top-8 raw logits at every step (teacher-forced reference for the bf16 engine)."""
+    t0 = time.time()
+    m = hf_model(LARGE_V3)
+    feats = features(LARGE_V3.num_mel_bins, B32_CASES)
+    out = {"cases": np.array([f"{k}:{s}" for k, s in B32_CASES]), "max_length": 128}
+    with torch.no_grad():
+        enc = torch.cat([m.model.encoder(feats[i: i + 8]).last_hidden_state for i in range(0, 32, 8)])
+    out["enc_slice"] = enc[:, ::250, :].numpy().astype(np.float32)
+    out["enc_stats"] = np.stack([enc.double().sum((1, 2)).numpy(), (enc.double() ** 2).sum((1, 2)).numpy()], 1)
+    del enc
+    print(f"  large_v3_b32: encoder ({time.time() - t0:.1f}s)")
+    kw = dict(language="ja", task="transcribe", return_timestamps=False, max_length=128)
+    m.generation_config, _ = hf_gen_config(LARGE_V3)
+    res = run_generate(m, feats, return_dict_in_generate=True, output_scores=True, output_logits=True, **kw)
+    logits = torch.stack(res.logits, 1)
+    top = logits.topk(8, -1)
+    out["greedy_logits_top_idx"] = top.indices.numpy().astype(np.int32)
+    out["greedy_logits_top_val"] = top.values.numpy().astype(np.float32)
+    del logits, top
+    s2 = torch.stack(res.scores, 1).topk(2, -1).values
+    out["greedy_margin"] = (s2[..., 0] - s2[..., 1]).numpy().astype(np.float32)
+    out["greedy_sequences"] = res.sequences.numpy().astype(np.int64)
+    del res, s2
+    print(f"  large_v3_b32: dict generate ({time.time() - t0:.1f}s)")
+    m.generation_config, _ = hf_gen_config(LARGE_V3)
+    out["greedy_tokens"] = run_generate(m, feats, **kw).numpy().astype(np.int64)
+    np.savez_compressed(os.path.join(GOLD, "large_v3_b32_fp32.npz"), **out)
+    print(f"large_v3_b32 fixtures done in {time.time() - t0:.1f}s {out['greedy_tokens'].shape}")
+
+
+KOTOBA_BEAM_CASES = [("tone", 0), ("dummy", 0), ("tone", 2), ("dummy", 3)]
+KOTOBA_BEAM_MODES = [
+    ("beam5_ts", dict(language="ja", task="transcribe", return_timestamps=True, num_beams=5, max_length=48)),
+    ("beam5", dict(language="ja", task="transcribe", return_timestamps=False, num_beams=5, max_length=48)),
+]
+
+
+def kotoba_beam_fixtures():
+    """tests/golden/kotoba_v2_beam_fp32.npz: BASELINE config 5's decode mode on the kotoba-whisper-v2.0
+    layout (32 encoder / 2 decoder layers, script/distil_whisper_v2.0.sh:130-134): beam 5 with and without
+    timestamps through the real HF generate (fp32, CPU)."""
+    t0 = time.time()
+    m = hf_model(KOTOBA_V2)
+    feats = features(KOTOBA_V2.num_mel_bins, KOTOBA_BEAM_CASES)
+    out = {"cases": np.array([f"{k}:{s}" for k, s in KOTOBA_BEAM_CASES])}
+    for name, kw in KOTOBA_BEAM_MODES:
+        m.generation_config, _ = hf_gen_config(KOTOBA_V2)
+        out[f"{name}_tokens"] = run_generate(m, feats, **kw).numpy().astype(np.int64)
+        print(f"  kotoba_v2_beam:{name} {out[f'{name}_tokens'].shape} ({time.time() - t0:.1f}s)")
+    np.savez_compressed(os.path.join(GOLD, "kotoba_v2_beam_fp32.npz"), **out)
+
+
+class _RecordingGenerate:
+    """Wraps ``model.generate`` to keep every window batch the pipeline hands it (tokens as returned)."""
+
+    def __init__(self, m):
+        self.m, self.orig, self.calls = m, m.generate, []
+
+    def __call__(self, *a, **kw):
+        res = self.orig(*a, **kw)
+        seq = res if isinstance(res, torch.Tensor) else res["sequences"]
+        self.calls.append(seq.numpy().astype(np.int64))
+        return res
+
+
+def _stub_tokenizer(gen):
+    """A stand-in tokenizer for the real ``AutomaticSpeechRecognitionPipeline`` (no vocab files offline):
+    ids decode to "[id]" strings; the special ids and ``_decode_asr`` are transformers' own
+    (tests/test_pipeline.py StubTokenizer)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import transformers.models.whisper.tokenization_whisper as tw
+    from test_pipeline import StubTokenizer
+
+    class Tok(StubTokenizer):
+        pad_token_id = gen.pad_token_id
+        eos_token_id = gen.eos_token_id
+        padding_side = "right"
+
+        def _decode_asr(self, model_outputs, *, return_timestamps, return_language, time_precision):
+            return tw._decode_asr(self, model_outputs, return_timestamps=return_timestamps,
+                                  return_language=return_language, time_precision=time_precision)
+
+    tk = Tok(gen)
+    tk.all_special_ids = tk.all_special_ids + [gen.pad_token_id]
+    return tk
+
+
+def pipeline_audio(spec):
+    """"kind:seed:seconds" -> the seeded 30 s clips of ``kind`` concatenated and cut (long_audio)."""
+    kind, seed, sec = str(spec).split(":")
+    return long_audio(kind, int(seed), float(sec))
+
+
+PIPE_CASES = {
+    # tag: (shape, clips, chunk_length_s, batch_size, generate_kwargs, return_timestamps values)
+    "tiny": (TINY, ["dummy:0:40", "dummy:0:7"], 15, 3, dict(language="ja", task="transcribe", max_length=40),
+             (False, True)),
+    # no chunk_length_s: > 30 s clips go through the long-form seek loop, one item each (batched, masks)
+    # (batch_size 1: transformers 5.15 cannot collate long-form items of different lengths, base.py:118)
+    "tiny_longform": (TINY, [f"{k}:{s}:{sec}" for k, s, sec in LONG_CLIPS], None, 1,
+                      dict(language="ja", task="transcribe"), (True,)),
+    # BASELINE config 5 (run_short_form_eval.py:110-117,184-191 with chunk_length 15): kotoba-v2.0, beam 5
+    "kotoba_v2": (KOTOBA_V2, ["tone:1:40", "dummy:5:12"], 15, 4,
+                  dict(language="ja", task="transcribe", num_beams=5, max_length=40), (True,)),
+}
+
+
+def pipeline_fixtures(tags=("tiny", "tiny_longform", "kotoba_v2")):
+    """tests/golden/pipeline_<tag>_fp32.npz: the REAL transformers ``pipeline("automatic-speech-recognition",
+    chunk_length_s=..., batch_size=...)`` (automatic_speech_recognition.py:61-84,432-447,483-598) over the
+    seeded HF model, with a stub tokenizer.  Stores the pipeline's final text / chunks (JSON) and every
+    window batch's generate output."""
+    from transformers import pipeline as hf_pipeline
+
+    for tag in tags:
+        t0 = time.time()
+        shape, clips, chunk_s, bs, gk, ts_modes = PIPE_CASES[tag]
+        m = hf_model(shape)
+        m.generation_config, gen = hf_gen_config(shape)
+        rec = _RecordingGenerate(m)
+        m.generate = rec
+        fe = WhisperFeatureExtractor(feature_size=shape.num_mel_bins)
+        pipe = hf_pipeline("automatic-speech-recognition", model=m, tokenizer=_stub_tokenizer(gen),
+                           feature_extractor=fe, chunk_length_s=chunk_s, batch_size=bs, device="cpu")
+        out = {"clips": np.array(clips), "batch_size": bs, "chunk_length_s": chunk_s or 0,
+               "generate_kwargs": np.array(json.dumps(gk))}
+        audio = [pipeline_audio(c) for c in clips]
+        for ts in ts_modes:
+            rec.calls.clear()
+            with torch.no_grad():
+                res = pipe([{"array": a, "sampling_rate": 16000} for a in audio], generate_kwargs=dict(gk),
+                           return_timestamps=ts)
+            key = f"ts{int(ts)}"
+            out[f"{key}_result"] = np.array(json.dumps(res))
+            out[f"{key}_n_calls"] = len(rec.calls)
+            for i, c in enumerate(rec.calls):
+                out[f"{key}_call{i}"] = c
+            print(f"  pipeline_{tag}:{key} {len(rec.calls)} window batches ({time.time() - t0:.1f}s)")
+        np.savez_compressed(os.path.join(GOLD, f"pipeline_{tag}_fp32.npz"), **out)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
@@ -251,6 +402,12 @@ def main():
         modes = [{"name": "greedy", "kw": dict(base, return_timestamps=False), "scores": True},
                  {"name": "greedy_ts", "kw": dict(base, return_timestamps=True, max_length=24)}]
         model_fixtures(LARGE_V3, "large_v3_fp32", cases, 32, modes)
+    if not a.skip_large and a.only in (None, "large_b32"):
+        large_b32_fixtures()
+    if not a.skip_large and a.only in (None, "kotoba_beam"):
+        kotoba_beam_fixtures()
+    if a.only in (None, "pipeline"):
+        pipeline_fixtures(("tiny", "tiny_longform") if a.skip_large else ("tiny", "tiny_longform", "kotoba_v2"))
     if not a.skip_large and a.only in (None, "kotoba"):
         cases = [("tone", 1), ("dummy", 2)]
         modes = [{"name": "greedy", "kw": dict(base, return_timestamps=False), "scores": True}]
