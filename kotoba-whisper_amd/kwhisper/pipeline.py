@@ -20,6 +20,7 @@ text field holds token-id lists instead of strings.  Host code only: the per-chu
 """
 from __future__ import annotations
 
+import copy
 from collections import defaultdict
 from typing import Callable, Iterable, List, Optional, Sequence
 
@@ -225,7 +226,25 @@ class ASRPipeline:
         self.batch_size = max(1, int(batch_size))
         self.generate_kwargs = dict(generate_kwargs or {})
         self.return_timestamps = return_timestamps
-        self.generation_config = model.generation_config
+        self.generation_config = self._pipeline_generation_config(model.generation_config)
+
+    # the ASR pipeline's own generation defaults (TF/pipelines/automatic_speech_recognition.py:160-163)
+    DEFAULT_MAX_NEW_TOKENS = 256
+    DEFAULT_NUM_BEAMS = 5  # "follows openai's whisper implementation"
+
+    @classmethod
+    def _pipeline_generation_config(cls, model_gen):
+        """The generation config the reference pipeline hands to every generate() call (TF/pipelines/base.py:
+        886-907 via GenerationMixin._prepare_generation_config, TF/generation/utils.py): the pipeline defaults
+        ``max_new_tokens=256, num_beams=5`` are the base and the model's generation config only fills fields
+        they leave unset -- so the pipeline decodes with 5 beams (BASELINE config 5's beam=5) unless the call
+        passes ``num_beams``; and ``max_new_tokens`` is dropped again when the model sets a non-default
+        ``max_length`` (Whisper's 448), which then bounds the decode."""
+        gen = model_gen.copy() if hasattr(model_gen, "copy") else copy.deepcopy(model_gen)
+        gen.num_beams = cls.DEFAULT_NUM_BEAMS
+        max_length = getattr(gen, "max_length", None)
+        gen.pipeline_max_new_tokens = None if (max_length is not None and max_length != 20) else cls.DEFAULT_MAX_NEW_TOKENS
+        return gen
 
     # ---- token vocabulary facts _decode_asr needs ------------------------------------------------------
     def _vocab(self):
@@ -347,6 +366,9 @@ class ASRPipeline:
         if rt:
             gk["return_timestamps"] = True
         gk.setdefault("generation_config", self.generation_config)
+        mnt = getattr(gk["generation_config"], "pipeline_max_new_tokens", None)
+        if mnt is not None and "max_length" not in gk and "max_new_tokens" not in gk:
+            gk["max_new_tokens"] = mnt
         fe = self.feature_extractor
         tokens = [None] * len(flat)
         for b0 in range(0, len(flat), bs):

@@ -28,8 +28,10 @@ from kwhisper.synthetic import synthetic_state_dict  # noqa: E402
 
 from _util import OracleFeatureExtractor, StubTok, clip_audio, jsonable, oracle_features  # noqa: E402
 
-# bf16 noise floor for greedy tokens: a step whose fp32 top-1/top-2 margin is below this may flip under
-# bf16 arithmetic (the measured teacher-forced logit error at large-v3 is printed by the test below)
+# bf16 noise floor for greedy tokens: a step whose fp32 top-1/top-2 margin is below this may flip under bf16
+# arithmetic.  The engine's measured teacher-forced logit error at config 3 is max 0.097 (r02b); the
+# reference's own bf16 model errs up to 0.19 and its greedy tokens already leave the fp32 ones at a 0.024
+# margin (tests/golden/large_v3_bf16ref.npz, row 0, step 21).
 MARGIN_FLOOR = 0.1
 
 
@@ -73,9 +75,16 @@ def large_b32_gold(gold):
     return g, oracle_features(LARGE_V3, g["cases"])
 
 
-def test_config3_bf16_generate_b32(large_b32_gold):
-    """The measured bf16 path at the bench's exact shape: B = 32, 128 graph-replayed decode steps."""
+def test_config3_bf16_generate_b32(gold, large_b32_gold):
+    """The measured bf16 path at the bench's exact shape: B = 32, 128 graph-replayed decode steps.
+
+    Tolerances are the REFERENCE's own bf16 noise (tests/golden/large_v3_bf16ref.npz: the same HF model cast to
+    bf16, as run_pseudo_labelling.py:229,338 runs it, on rows 0 and 16): on those rows the engine's encoder
+    and teacher-forced logits must be at least as close to fp32 as the reference's bf16 model is (x1.25 for
+    the encoder, whose bf16 rounding points differ); over all 32 rows the logit error bars are absolute."""
     g, feats_np = large_b32_gold
+    r = gold("large_v3_bf16ref")
+    rows = [int(x) for x in r["rows"]]
     model = _model(LARGE_V3, torch.bfloat16)
     feats = torch.from_numpy(feats_np).cuda()
     eng = model.engine
@@ -83,10 +92,16 @@ def test_config3_bf16_generate_b32(large_b32_gold):
     enc = eng.encode(feats)
     e = enc.view(32, 1500, 1280).float().cpu().numpy()[:, ::250, :]
     ref = g["enc_slice"]
-    rel = np.abs(e - ref).max() / np.abs(ref).max()
-    rel_mean = np.abs(e - ref).mean() / np.abs(ref).mean()
-    print(f"\nconfig3 bf16 encoder: max |err| / max |ref| = {rel:.4f}, mean |err| / mean |ref| = {rel_mean:.4f}")
-    assert rel < 0.05 and rel_mean < 0.01
+
+    def enc_err(x, y):
+        return np.abs(x - y).max() / np.abs(y).max(), np.abs(x - y).mean() / np.abs(y).mean()
+
+    ours_all, ours, theirs = enc_err(e, ref), enc_err(e[rows], ref[rows]), enc_err(r["enc_slice"], ref[rows])
+    print(f"\nconfig3 bf16 encoder vs fp32 reference (max|err|/max|ref|, mean|err|/mean|ref|): all 32 rows "
+          f"{ours_all[0]:.4f} / {ours_all[1]:.4f}; rows {rows}: engine {ours[0]:.4f} / {ours[1]:.4f}, "
+          f"reference bf16 model {theirs[0]:.4f} / {theirs[1]:.4f}")
+    assert ours[0] <= 1.25 * theirs[0] and ours[1] <= 1.25 * theirs[1]
+    assert ours_all[0] < 0.05 and ours_all[1] < 0.02
     # teacher-forced logits through the production decode kernels (packed weights, folded LayerNorms, LM head)
     sess = eng.new_session(32, enc)
     seq = torch.from_numpy(g["greedy_sequences"])
@@ -96,9 +111,13 @@ def test_config3_bf16_generate_b32(large_b32_gold):
     err = np.abs(got - g["greedy_logits_top_val"])
     top1 = lg[:, : idx.shape[1]].argmax(-1).cpu().numpy()
     agree = (top1 == g["greedy_logits_top_idx"][..., 0]).mean()
+    ref_err = np.abs(r["tf_logits_at_fp32_top8"] - g["greedy_logits_top_val"][rows])
     print(f"config3 bf16 teacher-forced top-8 logit err over {err.size} values: max {err.max():.4f} "
-          f"mean {err.mean():.5f} p99 {np.percentile(err, 99):.4f}; top-1 agreement {agree:.4f}")
-    assert err.max() < 0.35 and err.mean() < 0.03
+          f"mean {err.mean():.5f} p99 {np.percentile(err, 99):.4f}; top-1 agreement {agree:.4f}; on rows {rows}: "
+          f"engine max {err[rows].max():.4f} mean {err[rows].mean():.5f}, reference bf16 model max "
+          f"{ref_err.max():.4f} mean {ref_err.mean():.5f}")
+    assert err[rows].max() <= ref_err.max() and err[rows].mean() <= ref_err.mean()
+    assert err.max() < 0.2 and err.mean() < 0.03
     del lg, sess
     _free()
     # the graph-replayed generate() (what bench.py times)
@@ -285,13 +304,31 @@ def test_pipeline_chunked_tiny_vs_reference(gold, tiny32, fe_kind):
     _check_pipeline(gold("pipeline_tiny_fp32"), tiny32, TINY, fe_kind)
 
 
-@pytest.mark.parametrize("bs", [1, 3])
-def test_pipeline_longform_tiny_vs_reference(gold, tiny32, bs):
+def test_pipeline_longform_tiny_vs_reference(gold, tiny32):
     """ASRPipeline without chunking on 45 / 70 / 12 s clips: each item one long-form generate (the seek
-    loop) == transformers' pipeline at batch_size 1 (tests/golden/pipeline_tiny_longform_fp32.npz; at
-    batch_size > 1 transformers 5.15 cannot collate long-form items of different lengths, so batch 3 is
-    held to the same output)."""
-    _check_pipeline(gold("pipeline_tiny_longform_fp32"), tiny32, TINY, "oracle", batch_size=None if bs == 1 else bs)
+    loop; the pipeline's default beam 5) == transformers' pipeline at batch_size 1
+    (tests/golden/pipeline_tiny_longform_fp32.npz)."""
+    _check_pipeline(gold("pipeline_tiny_longform_fp32"), tiny32, TINY, "oracle")
+
+
+def test_pipeline_longform_tiny_batched(gold, tiny32):
+    """The same clips at batch_size 3 (transformers 5.15 cannot collate long-form items of different lengths,
+    pipelines/base.py:118, so this batch has no reference): the two > 30 s clips, which take the long-form
+    path either way, give the batch-1 reference's output; the 12 s clip, which batched becomes a masked
+    long-form item instead of one 30 s window, only has to run."""
+    from kwhisper.pipeline import ASRPipeline
+
+    g = gold("pipeline_tiny_longform_fp32")
+    gk = json.loads(str(g["generate_kwargs"]))
+    pipe = ASRPipeline(tiny32, feature_extractor=OracleFeatureExtractor(TINY.num_mel_bins),
+                       tokenizer=StubTok(generation_constants(TINY)), batch_size=3, generate_kwargs=gk)
+    got = jsonable(pipe([{"array": clip_audio(c), "sampling_rate": 16000} for c in g["clips"]], return_timestamps=True))
+    want = json.loads(str(g["ts1_result"]))
+    long_items = [i for i, c in enumerate(g["clips"]) if float(str(c).split(":")[2]) > 30]
+    assert long_items == [0, 1]
+    for i in long_items:
+        assert got[i] == want[i], i
+    assert len(got[2]["text"]) > 0
 
 
 # ---------------------------------------------------------------------------------------------------------
@@ -351,7 +388,8 @@ def test_config4_pseudo_label_engine(gold, tiny32, tmp_path):
         want = tiny32.generate(_item_features(idx), **GEN_KW).cpu().numpy()
         got = np.stack([preds1[i] for i in idx])
         np.testing.assert_array_equal(got, want)
-    fx = tiny32.generate(_item_features(range(4)), language="ja", task="transcribe", return_timestamps=True).cpu().numpy()
+    fx = tiny32.generate(_item_features(range(4)), language="ja", task="transcribe", return_timestamps=True,
+                         max_length=int(g["max_length"])).cpu().numpy()
     np.testing.assert_array_equal(fx, g["greedy_ts_tokens"])  # the loop's inputs are the pinned clips
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

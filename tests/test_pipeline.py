@@ -157,3 +157,35 @@ def test_decode_asr_token_mode():
     v["decode"] = None
     toks, _ = decode_asr(outputs, return_timestamps=False, time_precision=0.02, **v)
     assert text == tk.decode(toks)
+
+
+def test_pipeline_generation_defaults_match_transformers():
+    """ASRPipeline decodes with the generation config transformers' pipeline builds (base.py:886-907 over
+    automatic_speech_recognition.py:160-163): beam 5 by default, max_new_tokens dropped for Whisper's
+    max_length 448 and kept (256) when the model leaves max_length at the global default."""
+    import torch
+    from transformers import GenerationConfig, WhisperConfig, WhisperFeatureExtractor, WhisperForConditionalGeneration
+    from transformers import pipeline as hf_pipeline
+
+    from kwhisper.pipeline import ASRPipeline
+
+    cfg = WhisperConfig(vocab_size=51865, d_model=64, encoder_layers=1, decoder_layers=1, encoder_attention_heads=1,
+                        decoder_attention_heads=1, encoder_ffn_dim=64, decoder_ffn_dim=64)
+    m = WhisperForConditionalGeneration(cfg).eval()
+    for max_length in (448, None):
+        d = {k: v for k, v in G.to_dict().items() if k not in ("language", "task")}
+        d["max_length"] = max_length
+        if max_length is None:
+            d.pop("max_length")
+        m.generation_config = GenerationConfig(**d)
+
+        class _Tok(StubTokenizer):
+            pad_token_id, eos_token_id, padding_side = G.pad_token_id, G.eos_token_id, "right"
+
+        p = hf_pipeline("automatic-speech-recognition", model=m, tokenizer=_Tok(), feature_extractor=WhisperFeatureExtractor(),
+                        device="cpu")
+        ours = G.copy()
+        ours.max_length = max_length
+        got = ASRPipeline._pipeline_generation_config(ours)
+        assert got.num_beams == p.generation_config.num_beams == 5
+        assert got.pipeline_max_new_tokens == p.generation_config.max_new_tokens, max_length

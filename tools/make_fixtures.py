@@ -257,6 +257,34 @@ def large_b32_fixtures():
     print(f"large_v3_b32 fixtures done in {time.time() - t0:.1f}s {out['greedy_tokens'].shape}")
 
 
+def large_bf16_ref_fixtures(rows=(0, 16)):
+    """tests/golden/large_v3_bf16ref.npz: the REFERENCE's own bf16 noise floor at config 3.  The reference
+    runs its teacher in bfloat16 (run_pseudo_labelling.py:229,338); here the same HF model is cast to bf16 on
+    CPU and run on two of the config-3 clips: its encoder output, its teacher-forced logits on the fp32
+    reference's token sequence (one decoder pass, at the fp32 top-8 ids) and its own greedy tokens.  The
+    bf16 engine's tolerances are stated relative to these (tests/test_gpu_workloads.py)."""
+    t0 = time.time()
+    g = np.load(os.path.join(GOLD, "large_v3_b32_fp32.npz"))
+    cases = [B32_CASES[r] for r in rows]
+    m = hf_model(LARGE_V3).to(torch.bfloat16)
+    feats = features(LARGE_V3.num_mel_bins, cases).to(torch.bfloat16)
+    out = {"rows": np.array(rows), "cases": np.array([f"{k}:{s}" for k, s in cases])}
+    with torch.no_grad():
+        enc = m.model.encoder(feats).last_hidden_state
+        out["enc_slice"] = enc[:, ::250, :].float().numpy()
+        print(f"  large_v3_bf16ref: encoder ({time.time() - t0:.1f}s)")
+        seq = torch.from_numpy(g["greedy_sequences"][list(rows), :-1])
+        lg = m(encoder_outputs=(enc,), decoder_input_ids=seq).logits.float()[:, 3:]  # predicts seq[:, 4:] + 1
+        idx = torch.from_numpy(g["greedy_logits_top_idx"][list(rows)].astype(np.int64))
+        out["tf_logits_at_fp32_top8"] = torch.gather(lg[:, : idx.shape[1]], -1, idx).numpy().astype(np.float32)
+        print(f"  large_v3_bf16ref: teacher-forced logits ({time.time() - t0:.1f}s)")
+    m.generation_config, _ = hf_gen_config(LARGE_V3)
+    out["greedy_tokens"] = run_generate(m, feats, language="ja", task="transcribe", return_timestamps=False,
+                                        max_length=128).numpy().astype(np.int64)
+    np.savez_compressed(os.path.join(GOLD, "large_v3_bf16ref.npz"), **out)
+    print(f"large_v3_bf16ref fixtures done in {time.time() - t0:.1f}s")
+
+
 KOTOBA_BEAM_CASES = [("tone", 0), ("dummy", 0), ("tone", 2), ("dummy", 3)]
 KOTOBA_BEAM_MODES = [
     ("beam5_ts", dict(language="ja", task="transcribe", return_timestamps=True, num_beams=5, max_length=48)),
@@ -404,6 +432,8 @@ def main():
         model_fixtures(LARGE_V3, "large_v3_fp32", cases, 32, modes)
     if not a.skip_large and a.only in (None, "large_b32"):
         large_b32_fixtures()
+    if not a.skip_large and a.only in (None, "large_bf16ref"):
+        large_bf16_ref_fixtures()
     if not a.skip_large and a.only in (None, "kotoba_beam"):
         kotoba_beam_fixtures()
     if a.only in (None, "pipeline"):
