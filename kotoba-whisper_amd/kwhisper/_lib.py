@@ -14,6 +14,11 @@ import os
 import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
 
 LIB_PATH = os.environ.get("KWHISPER_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libkwhisper.so")
+# torch.ops.kw.* (csrc/torch_ops.cpp), linked against libkwhisper.so found beside it
+TORCH_LIB_PATH = os.environ.get("KWHISPER_TORCH_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
+                                                                      "libkwhisper_torch.so")
+TORCH_OPS = ("log_mel", "mel_to_time_major", "gemm", "dec_linear", "pack_weight", "layernorm", "attention", "embed",
+             "self_attn_step", "cross_attn_step", "greedy_step", "beam_logprobs", "beam_select")
 
 KW_OK, KW_EINVAL, KW_EHIP, KW_EUNSUPPORTED = 0, 1, 2, 3
 KW_DT_F32, KW_DT_BF16 = 0, 1
@@ -140,6 +145,33 @@ def load(path: str = LIB_PATH):
         fn.argtypes = args
     _lib = lib
     return lib
+
+
+_torch_ops = None
+
+
+def load_torch_ops(path: str = TORCH_LIB_PATH):
+    """Load the PyTorch custom-op library once and return ``torch.ops.kw``; raises if it is missing (no
+    fallback path exists).  Registers fake (meta) implementations so torch.compile / export can trace the
+    ops: each mutates its output tensors in place and returns nothing."""
+    global _torch_ops
+    if _torch_ops is not None:
+        return _torch_ops
+    if not os.path.exists(path):
+        raise KWError(
+            f"kwhisper torch-op library not found at {path}; build it with `make -C kotoba-whisper_amd/csrc` or "
+            "`python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    load()  # the C ABI library first (same HIP runtime, its last-error state is shared)
+    torch.ops.load_library(path)
+    kw = torch.ops.kw
+    for name in TORCH_OPS:
+        try:
+            torch.library.register_fake(f"kw::{name}")(lambda *a, **k: None)
+        except RuntimeError:  # already registered (library re-loaded in this process)
+            pass
+    _torch_ops = kw
+    return kw
 
 
 def check(rc: int, what: str) -> None:

@@ -1,8 +1,8 @@
 """WhisperEngine: weights in HBM, the encoder pass and device-resident decode sessions.
 
 Mirrors the compute of ``WhisperForConditionalGeneration`` (TF/models/whisper/modeling_whisper.py):
-encoder :592-646, decoder :690-795, proj_out :1080.  Every op is a kwhisper HIP kernel through the
-C ABI; torch only owns memory, streams and graph capture.
+encoder :592-646, decoder :690-795, proj_out :1080.  Every op is a kwhisper HIP kernel launched through
+the ``torch.ops.kw`` custom ops over the C ABI; torch only owns memory, streams and graph capture.
 
 Layout in HBM (DESIGN.md §Data layout):
   * encoder residual stream [rows][d]: bf16 on the bf16 path (the reference's bf16 model keeps it in
@@ -66,6 +66,7 @@ class WhisperEngine:
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
         L.load()
+        L.load_torch_ops()  # torch.ops.kw.* (the launch path of every op); raises if it was not built
         self.shape = shape
         self.dtype = dtype
         self.device = torch.device(device)

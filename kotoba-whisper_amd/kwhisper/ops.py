@@ -1,10 +1,15 @@
-"""Torch-tensor front end of the kwhisper C ABI.
+"""Torch-tensor front end of the kwhisper C ABI, through the PyTorch-ROCm custom ops ``torch.ops.kw.*``.
 
-Each function validates shapes/dtypes/devices, then launches on the current
-torch stream.  Tensors are plumbing only (device memory + stream); all
-arithmetic happens in the HIP kernels of ``libkwhisper.so``.  ``GemmPlan`` /
-``GemvPlan`` pre-build the C argument block once so decode steps can be
-replayed (and hipGraph-captured) without Python-side re-validation.
+Every launch goes through a ``torch.ops.kw`` operator (``csrc/torch_ops.cpp``, SURVEY.md §8b: "Torch custom
+ops wrap the ABI"), which fills the C ABI's argument block and launches on torch's current HIP stream, so
+the kernels are ordinary torch ops to the dispatcher, to ``torch.cuda.graph`` capture and to
+``torch.compile`` (fake implementations are registered: every op mutates its outputs and returns nothing).
+Tensors are plumbing only (device memory + stream); all arithmetic happens in the HIP kernels of
+``libkwhisper.so``.  The plan classes (``GemmPlan``, ``DecLinearPlan``, ``SamplerPlan``, ``BeamStepPlan``)
+validate once and keep the op arguments, so decode steps replay without re-validation.
+
+``set_backend("ctypes")`` routes the same calls through the ctypes binding of the C ABI instead (used by
+the test that holds the two paths bitwise equal); there is no CPU or torch fallback on either path.
 """
 from __future__ import annotations
 
@@ -15,6 +20,25 @@ import torch
 from . import _lib as L
 
 _DT = {torch.float32: L.KW_DT_F32, torch.bfloat16: L.KW_DT_BF16}
+_BACKEND = "torch"
+
+
+def set_backend(name: str) -> str:
+    """Select "torch" (torch.ops.kw, the default) or "ctypes" (the C ABI bound directly); returns the old one."""
+    global _BACKEND
+    if name not in ("torch", "ctypes"):
+        raise ValueError("backend must be 'torch' or 'ctypes'")
+    old, _BACKEND = _BACKEND, name
+    return old
+
+
+def backend() -> str:
+    return _BACKEND
+
+
+def _kw():
+    """The torch.ops.kw namespace (loads libkwhisper_torch.so once; raises if it is missing)."""
+    return L.load_torch_ops()
 
 
 def _lib():
@@ -42,6 +66,15 @@ def _cuda(*ts):
             raise ValueError("kwhisper ops take device (cuda) tensors")
 
 
+def _ws_bytes(kind: str, *dims) -> int:
+    if _BACKEND == "torch":
+        return int(_kw().workspace_bytes(kind, [int(d) for d in dims]))
+    fn = {"dec_linear": "kw_dec_linear_workspace_bytes", "packed_weight": "kw_packed_weight_bytes",
+          "self_attn": "kw_self_attn_workspace", "cross_attn": "kw_cross_attn_workspace",
+          "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace"}[kind]
+    return int(getattr(_lib(), fn)(*dims))
+
+
 def log_mel(audio: torch.Tensor, mel_filters: torch.Tensor, out: torch.Tensor | None = None,
             workspace: torch.Tensor | None = None) -> torch.Tensor:
     """audio (B, n) f32, n % 160 == 0 -> (B, n_mels, n // 160) f32 log-mel."""
@@ -56,8 +89,11 @@ def log_mel(audio: torch.Tensor, mel_filters: torch.Tensor, out: torch.Tensor | 
         out = torch.empty((b, n_mels, n // 160), device=audio.device, dtype=torch.float32)
     if workspace is None:
         workspace = torch.empty((max(b, 1),), device=audio.device, dtype=torch.int32)
-    L.check(_lib().kw_log_mel(_p(audio), b, n, audio.stride(0), _p(mel_filters), n_mels, _p(out), _p(workspace), _s()),
-            "kw_log_mel")
+    if _BACKEND == "torch":
+        _kw().log_mel(audio, mel_filters, out, workspace)
+    else:
+        L.check(_lib().kw_log_mel(_p(audio), b, n, audio.stride(0), _p(mel_filters), n_mels, _p(out), _p(workspace),
+                                  _s()), "kw_log_mel")
     return out
 
 
@@ -66,8 +102,11 @@ def mel_to_time_major(mel: torch.Tensor, c_pad: int, dtype: torch.dtype, out: to
     b, c, t = mel.shape
     if out is None:
         out = torch.empty((b, t + 2, c_pad), device=mel.device, dtype=dtype)
-    L.check(_lib().kw_mel_to_time_major(_p(mel.contiguous()), b, c, t, c_pad, _p(out), _DT[dtype], _s()),
-            "kw_mel_to_time_major")
+    mel = mel.contiguous()
+    if _BACKEND == "torch":
+        _kw().mel_to_time_major(mel, c_pad, out)
+    else:
+        L.check(_lib().kw_mel_to_time_major(_p(mel), b, c, t, c_pad, _p(out), _DT[dtype], _s()), "kw_mel_to_time_major")
     return out
 
 
@@ -80,6 +119,9 @@ def layernorm(x: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: flo
         raise ValueError("layernorm input must be contiguous float32 or bfloat16")
     if delta is not None and (delta.dtype != torch.bfloat16 or delta.numel() != x.numel() or not delta.is_contiguous()):
         raise ValueError("layernorm delta must be a contiguous bf16 tensor of x's size")
+    if _BACKEND == "torch":
+        _kw().layernorm(x, gamma, beta, float(eps), out, delta)
+        return out
     dim = x.shape[-1]
     rows = x.numel() // dim
     if x.dtype == torch.bfloat16:
@@ -99,20 +141,27 @@ class GemmPlan:
                  scale=1.0, scale_cols=0, row_add=None, row_add_period=0, hs_seq=0, hs_heads=0, hs_head_dim=0,
                  dtype=None, a_offset=0, c_offset=0):
         _cuda(A, W, C, bias, row_add)
+        if bias is not None and bias.dtype != torch.float32:
+            raise ValueError("bias must be float32")
+        if row_add is not None and row_add.dtype != torch.float32:
+            raise ValueError("row_add must be float32")
+        lda = K if lda is None else lda
+        ldc = N if ldc is None else ldc
         self._keep = (A, W, C, bias, row_add)
+        # torch.ops.kw.gemm arguments
+        self._geo = [a_offset, lda, a_rows_per_batch, a_batch_stride, c_offset, ldc, c_rows_per_batch, c_batch_stride,
+                     M, N, K, epilogue, int(bool(gelu)), scale_cols, row_add_period, hs_seq, hs_heads, hs_head_dim]
+        self._targs = (A, W, bias, C, row_add, self._geo, float(scale), -1 if dtype is None else _DT[dtype])
+        # the same call as a C argument block (ctypes backend)
         a = L.GemmArgs()
         a.dtype = _dt(W) if dtype is None else _DT[dtype]
         a.c_dtype = _dt(C)
         a.A = A.data_ptr() + a_offset * A.element_size()
-        a.lda = K if lda is None else lda
-        a.a_rows_per_batch = a_rows_per_batch
-        a.a_batch_stride = a_batch_stride
+        a.lda, a.a_rows_per_batch, a.a_batch_stride = lda, a_rows_per_batch, a_batch_stride
         a.W = W.data_ptr()
         a.bias = bias.data_ptr() if bias is not None else None
         a.C = C.data_ptr() + c_offset * C.element_size()
-        a.ldc = N if ldc is None else ldc
-        a.c_rows_per_batch = c_rows_per_batch
-        a.c_batch_stride = c_batch_stride
+        a.ldc, a.c_rows_per_batch, a.c_batch_stride = ldc, c_rows_per_batch, c_batch_stride
         a.M, a.N, a.K = M, N, K
         a.epilogue = epilogue
         a.gelu = int(bool(gelu))
@@ -121,19 +170,18 @@ class GemmPlan:
         a.row_add = row_add.data_ptr() if row_add is not None else None
         a.row_add_period = row_add_period
         a.hs_seq, a.hs_heads, a.hs_head_dim = hs_seq, hs_heads, hs_head_dim
-        if bias is not None and bias.dtype != torch.float32:
-            raise ValueError("bias must be float32")
-        if row_add is not None and row_add.dtype != torch.float32:
-            raise ValueError("row_add must be float32")
         self.args = a
         self._ref = ctypes.byref(a)
 
     def __call__(self):
-        L.check(_lib().kw_gemm(self._ref, _s()), "kw_gemm")
+        if _BACKEND == "torch":
+            _kw().gemm(*self._targs)
+        else:
+            L.check(_lib().kw_gemm(self._ref, _s()), "kw_gemm")
 
 
 def dec_linear_workspace_bytes(N: int, K: int) -> int:
-    return int(_lib().kw_dec_linear_workspace_bytes(N, K))
+    return _ws_bytes("dec_linear", N, K)
 
 
 class DecLinearPlan:
@@ -151,10 +199,12 @@ class DecLinearPlan:
             raise ValueError("kw_dec_linear takes bf16 activations and packed bf16 weights")
         if bias is not None and bias.dtype != torch.float32:
             raise ValueError("bias must be float32")
+        ldx = K if ldx is None else ldx
         a = L.DecLinearArgs()
         keep = [x, W, bias, C, workspace]
         a.x = x.data_ptr() + x_offset * 2
-        a.ldx = K if ldx is None else ldx
+        a.ldx = ldx
+        colsum, eps = None, 0.0
         if ln is not None:
             eps, colsum = ln
             _cuda(colsum)
@@ -166,6 +216,8 @@ class DecLinearPlan:
             keep.append(colsum)
         a.W = W.data_ptr()
         a.bias = bias.data_ptr() if bias is not None else None
+        h = hb = None
+        row0 = ldh = 0
         if resid is not None:
             h, hb, ldh, row0 = resid
             _cuda(h, hb)
@@ -176,12 +228,14 @@ class DecLinearPlan:
             a.hb = hb.data_ptr() + row0 * ldh * 2
             a.ldh = ldh
             keep += [h, hb]
+            C = None
         else:
             if C is None:
                 raise ValueError("STORE needs C")
             a.epilogue = L.KW_EPI_STORE
+            ldc = N if ldc is None else ldc
             a.C = C.data_ptr() + c_offset * C.element_size()
-            a.ldc = N if ldc is None else ldc
+            a.ldc = ldc
             a.c_dtype = _dt(C)
         a.gelu = int(bool(gelu))
         a.scale = float(scale)
@@ -196,11 +250,17 @@ class DecLinearPlan:
         a.workspace = workspace.data_ptr()
         a.ws_bytes = workspace.numel() * workspace.element_size()
         self._keep = tuple(keep)
+        geo = [x_offset, ldx, 1 if ln is not None else 0, c_offset, 0 if C is None else (ldc or N), int(bool(gelu)),
+               scale_cols, row0, ldh, M, N, K]
+        self._targs = (x, W, bias, colsum, C, h, hb, workspace, geo, float(eps), float(scale))
         self.args = a
         self._ref = ctypes.byref(a)
 
     def __call__(self):
-        L.check(_lib().kw_dec_linear(self._ref, _s()), "kw_dec_linear")
+        if _BACKEND == "torch":
+            _kw().dec_linear(*self._targs)
+        else:
+            L.check(_lib().kw_dec_linear(self._ref, _s()), "kw_dec_linear")
 
 
 def ln_colsum(W: torch.Tensor) -> torch.Tensor:
@@ -214,9 +274,12 @@ def pack_weight(W: torch.Tensor) -> torch.Tensor:
     if W.dtype != torch.bfloat16 or W.dim() != 2 or not W.is_contiguous():
         raise ValueError("pack_weight expects a contiguous 2-D bfloat16 tensor")
     n, k = W.shape
-    nbytes = _lib().kw_packed_weight_bytes(n, k)
+    nbytes = _ws_bytes("packed_weight", n, k)
     out = torch.empty((nbytes // 2,), device=W.device, dtype=torch.bfloat16)
-    L.check(_lib().kw_pack_weight(_p(W), n, k, _p(out), _s()), "kw_pack_weight")
+    if _BACKEND == "torch":
+        _kw().pack_weight(W, out)
+    else:
+        L.check(_lib().kw_pack_weight(_p(W), n, k, _p(out), _s()), "kw_pack_weight")
     return out
 
 
@@ -224,25 +287,34 @@ def attention(qkv: torch.Tensor, B: int, H: int, T: int, hd: int, out: torch.Ten
     _cuda(qkv, out)
     if qkv.numel() != 3 * B * H * T * hd or out.numel() != B * T * H * hd or qkv.dtype != out.dtype:
         raise ValueError("attention: qkv must hold [3][B][H][T][hd] and out [B][T][H*hd] of one dtype")
-    L.check(_lib().kw_attention(_dt(qkv), _p(qkv), B, H, T, hd, _p(out), _s()), "kw_attention")
+    if _BACKEND == "torch":
+        _kw().attention(qkv, B, H, T, hd, out)
+    else:
+        L.check(_lib().kw_attention(_dt(qkv), _p(qkv), B, H, T, hd, _p(out), _s()), "kw_attention")
     return out
 
 
 def embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h, hb=None):
     """Decoder embedding into the f32 residual h (and its bf16 mirror hb for the bf16 engine)."""
     _cuda(ids, cur_len, tok_emb, pos_emb, h, hb)
-    L.check(_lib().kw_embed(_dt(tok_emb), _p(ids), ids.stride(0), B, q_len, _p(cur_len), _p(tok_emb), _p(pos_emb),
-                            tok_emb.shape[1], _p(h), _p(hb), _s()), "kw_embed")
+    if _BACKEND == "torch":
+        _kw().embed(ids, B, q_len, cur_len, tok_emb, pos_emb, h, hb)
+    else:
+        L.check(_lib().kw_embed(_dt(tok_emb), _p(ids), ids.stride(0), B, q_len, _p(cur_len), _p(tok_emb), _p(pos_emb),
+                                tok_emb.shape[1], _p(h), _p(hb), _s()), "kw_embed")
 
 
 def self_attn_workspace_bytes(B, H, t_max) -> int:
-    return int(_lib().kw_self_attn_workspace(B, H, t_max))
+    return _ws_bytes("self_attn", B, H, t_max)
 
 
 def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out, workspace=None, bp=None):
     """Static-cache self-attention; q_len == 1 needs a zero-filled ``workspace`` (self_attn_workspace_bytes);
     ``bp``: beam-search slot table [B][>= t_max] int32 (q_len == 1)."""
     _cuda(qkv, k_cache, v_cache, cur_len, out, workspace, bp)
+    if _BACKEND == "torch":
+        _kw().self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out, workspace, bp)
+        return
     nb = workspace.numel() * workspace.element_size() if workspace is not None else 0
     L.check(_lib().kw_self_attn_step(_dt(qkv), _p(qkv), B, q_len, H, hd, _p(k_cache), _p(v_cache), t_max,
                                      _p(cur_len), _p(bp), bp.stride(0) if bp is not None else 0, _p(out),
@@ -250,21 +322,24 @@ def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out, 
 
 
 def cross_attn_workspace_bytes(B, q_len, H, hd, S) -> int:
-    return int(_lib().kw_cross_attn_workspace(B, q_len, H, hd, S))
+    return _ws_bytes("cross_attn", B, q_len, H, hd, S)
 
 
 def cross_attn_step(q, B, q_len, H, hd, k, v, S, out, workspace):
     _cuda(q, k, v, out, workspace)
+    if _BACKEND == "torch":
+        _kw().cross_attn_step(q, B, q_len, H, hd, k, v, S, out, workspace)
+        return
     L.check(_lib().kw_cross_attn_step(_dt(q), _p(q), B, q_len, H, hd, _p(k), _p(v), S, _p(out), _p(workspace),
                                       workspace.numel() * workspace.element_size(), _s()), "kw_cross_attn_step")
 
 
 def beam_logprobs_workspace_bytes(R: int) -> int:
-    return int(_lib().kw_beam_logprobs_workspace(R))
+    return _ws_bytes("beam_logprobs", R)
 
 
 def greedy_step_workspace_bytes(B: int) -> int:
-    return int(_lib().kw_greedy_step_workspace(B))
+    return _ws_bytes("greedy_step", B)
 
 
 class SamplerPlan:
@@ -277,6 +352,10 @@ class SamplerPlan:
               workspace)
         self._keep = (logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished, scores_out,
                       workspace)
+        mit = -1 if max_initial_ts is None else max_initial_ts
+        cfg = [int(bool(return_timestamps)), ts_begin, no_ts_id, eos_id, pad_id, mit, max_length, begin_index]
+        self._targs = (logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, counter, n_unfinished,
+                       scores_out, workspace, cfg)
         a = L.SamplerArgs()
         a.logits = logits.data_ptr()
         a.B, a.V = logits.shape
@@ -285,7 +364,7 @@ class SamplerPlan:
         a.n_begin_suppress = begin_suppress.numel() if begin_suppress is not None else 0
         a.return_timestamps = int(bool(return_timestamps))
         a.ts_begin, a.no_ts_id, a.eos_id, a.pad_id = ts_begin, no_ts_id, eos_id, pad_id
-        a.max_initial_ts = -1 if max_initial_ts is None else max_initial_ts
+        a.max_initial_ts = mit
         a.ids = ids.data_ptr()
         a.ids_stride = ids.stride(0)
         a.cur_len = cur_len.data_ptr()
@@ -301,7 +380,10 @@ class SamplerPlan:
         self._ref = ctypes.byref(a)
 
     def __call__(self):
-        L.check(_lib().kw_greedy_step(self._ref, _s()), "kw_greedy_step")
+        if _BACKEND == "torch":
+            _kw().greedy_step(*self._targs)
+        else:
+            L.check(_lib().kw_greedy_step(self._ref, _s()), "kw_greedy_step")
 
 
 class BeamStepPlan:
@@ -313,6 +395,15 @@ class BeamStepPlan:
         self._keep = (st, logits, suppress_mask, begin_suppress)
         R, V = logits.shape
         B, nb = st["fin_score"].shape
+        mit = -1 if max_initial_ts is None else max_initial_ts
+        es = 2 if early_stopping == "never" else int(bool(early_stopping))
+        ws = st.get("lp_ws")  # split-row log-probs / top-k (kw_beam_logprobs_workspace), zero-filled once
+        bp = st.get("bp")
+        self._tlp = (logits, suppress_mask, begin_suppress, st["ids"], st["cur_len"], st["cand_val"], st["cand_idx"],
+                     st["done"], ws, [int(bool(return_timestamps)), ts_begin, no_ts_id, eos_id, mit, begin_index, 2 * nb])
+        self._tsel = (st["cand_val"], st["cand_idx"], st["ids"], bp, st["run_scores"], st["fin_seq"], st["fin_score"],
+                      st["fin_len"], st["fin_flag"], st["unsat"], st["cur_len"], st["counter"], st["go"], st["done"],
+                      st["item_flags"], [B, nb, V, begin_index, max_length, eos_id, fill_id, es], float(length_penalty))
         a = L.BeamLogprobsArgs()
         a.logits, a.R, a.V = logits.data_ptr(), R, V
         a.suppress_mask = suppress_mask.data_ptr()
@@ -320,36 +411,40 @@ class BeamStepPlan:
         a.n_begin_suppress = begin_suppress.numel() if begin_suppress is not None else 0
         a.return_timestamps = int(bool(return_timestamps))
         a.ts_begin, a.no_ts_id, a.eos_id = ts_begin, no_ts_id, eos_id
-        a.max_initial_ts = -1 if max_initial_ts is None else max_initial_ts
+        a.max_initial_ts = mit
         a.ids, a.ids_stride = st["ids"].data_ptr(), st["ids"].stride(0)
         a.cur_len = st["cur_len"].data_ptr()
         a.begin_index = begin_index
         a.k = 2 * nb
         a.cand_val, a.cand_idx, a.done = st["cand_val"].data_ptr(), st["cand_idx"].data_ptr(), st["done"].data_ptr()
-        ws = st.get("lp_ws")  # split-row log-probs / top-k (kw_beam_logprobs_workspace), zero-filled once
         a.workspace = ws.data_ptr() if ws is not None else None
         a.ws_bytes = ws.numel() * ws.element_size() if ws is not None else 0
         b = L.BeamSelectArgs()
         b.B, b.num_beams, b.V = B, nb, V
         b.cand_val, b.cand_idx = a.cand_val, a.cand_idx
         b.ids, b.ids_stride = a.ids, a.ids_stride
-        b.bp = st["bp"].data_ptr() if st.get("bp") is not None else None
-        b.bp_stride = st["bp"].stride(0) if st.get("bp") is not None else 0
+        b.bp = bp.data_ptr() if bp is not None else None
+        b.bp_stride = bp.stride(0) if bp is not None else 0
         b.run_scores = st["run_scores"].data_ptr()
         b.fin_seq, b.fin_stride = st["fin_seq"].data_ptr(), st["fin_seq"].shape[-1]
         b.fin_score, b.fin_len, b.fin_flag = st["fin_score"].data_ptr(), st["fin_len"].data_ptr(), st["fin_flag"].data_ptr()
         b.unsat, b.cur_len = st["unsat"].data_ptr(), a.cur_len
         b.begin_index, b.max_length, b.eos_id, b.fill_id = begin_index, max_length, eos_id, fill_id
         b.length_penalty = float(length_penalty)
-        b.early_stopping = 2 if early_stopping == "never" else int(bool(early_stopping))
+        b.early_stopping = es
         b.counter, b.go, b.done = st["counter"].data_ptr(), st["go"].data_ptr(), a.done
         b.item_flags = st["item_flags"].data_ptr()
         self.a, self.b = a, b
         self._ra, self._rb = ctypes.byref(a), ctypes.byref(b)
 
     def __call__(self):
-        L.check(_lib().kw_beam_logprobs(self._ra, _s()), "kw_beam_logprobs")
-        L.check(_lib().kw_beam_select(self._rb, _s()), "kw_beam_select")
+        if _BACKEND == "torch":
+            kw = _kw()
+            kw.beam_logprobs(*self._tlp)
+            kw.beam_select(*self._tsel)
+        else:
+            L.check(_lib().kw_beam_logprobs(self._ra, _s()), "kw_beam_logprobs")
+            L.check(_lib().kw_beam_select(self._rb, _s()), "kw_beam_select")
 
 
 def cu_range_stream(cu_begin: int, cu_end: int) -> torch.cuda.ExternalStream:

@@ -73,3 +73,35 @@ def test_errors_are_returned_not_thrown(lib):
     rc = lib.kw_layernorm(None, 1, 7, None, None, 1e-5, None, 0, None, None)
     assert rc == 1
     assert b"kw_layernorm" in lib.kw_last_error()
+
+
+def test_torch_ops_register_every_entry_point(lib):
+    """torch.ops.kw (libkwhisper_torch.so) loads beside the C ABI and registers one operator per
+    launching entry point, each mutating its outputs in place (schema annotations) with a CUDA (HIP) kernel."""
+    import torch
+
+    from kwhisper import _lib
+
+    kw = _lib.load_torch_ops()
+    assert int(kw.version()) == lib.kw_version()
+    for name in _lib.TORCH_OPS:
+        schema = str(getattr(kw, name).default._schema)
+        assert schema.startswith(f"kw::{name}(") and schema.endswith("-> ()"), schema
+        assert "(a!)" in schema, schema
+        assert torch._C._dispatch_has_kernel_for_dispatch_key(f"kw::{name}", "CUDA"), name
+    assert int(kw.workspace_bytes("dec_linear", [1280, 5120])) == lib.kw_dec_linear_workspace_bytes(1280, 5120)
+    # ABI symbols bound by the torch library are the header's (no private re-implementation)
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.TORCH_LIB_PATH], capture_output=True, text=True).stdout
+    used = set(re.findall(r"\b(kw_[a-z0-9_]+)\b", out))
+    assert used and used <= set(_declared()), used - set(_declared())
+
+
+def test_torch_ops_reject_host_tensors(lib):
+    """No CPU path: a host tensor is refused with ValueError before any launch."""
+    import torch
+
+    from kwhisper import _lib
+
+    kw = _lib.load_torch_ops()
+    with pytest.raises((ValueError, NotImplementedError)):
+        kw.attention(torch.zeros(3 * 64), 1, 1, 1, 64, torch.zeros(64))

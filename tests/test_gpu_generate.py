@@ -237,3 +237,54 @@ def test_tiny_fp32_longform_bitexact(gold, tiny32):
     np.testing.assert_array_equal(plain.cpu().numpy(), g["long_ts_tokens"])
     single = tiny32.generate(torch.from_numpy(one).cuda(), language="ja", task="transcribe", return_timestamps=True)
     np.testing.assert_array_equal(single.cpu().numpy(), g["long_single_tokens"])
+
+
+def test_torch_ops_decode_graph_matches_ctypes(gold):
+    """SURVEY §8b boundary: the bf16 engine launched through torch.ops.kw (the default path) -- greedy
+    generate() with its prefill and step captured into hipGraphs, beam search, teacher-forced logits --
+    is bit for bit the engine launched through the ctypes binding of the same C ABI."""
+    from kwhisper import ops
+
+    g = gold("tiny_fp32")
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    seq = torch.from_numpy(g["greedy_sequences"])
+    res = {}
+    old = ops.backend()
+    try:
+        for be in ("torch", "ctypes"):
+            ops.set_backend(be)
+            m = _model(TINY, torch.bfloat16)  # fresh plans, sessions and graph captures per backend
+            toks = m.generate(feats, language="ja", task="transcribe", max_length=64).cpu()
+            beam = m.generate(feats, language="ja", task="transcribe", num_beams=3, max_length=24).cpu()
+            sess = m.engine.new_session(feats.shape[0], m.engine.encode(feats))
+            lg = sess.teacher_forced_logits(seq[:, :12], 4).cpu()
+            res[be] = (toks, beam, lg)
+            del m, sess
+    finally:
+        ops.set_backend(old)
+    for a, b in zip(res["torch"], res["ctypes"]):
+        assert torch.equal(a, b)
+
+
+def test_torch_ops_trace_under_torch_compile():
+    """The custom ops are visible to torch.compile (fake implementations registered): a compiled function
+    calling torch.ops.kw.layernorm / attention traces with fullgraph=True and equals the eager call."""
+    from kwhisper import _lib
+
+    kw = _lib.load_torch_ops()
+    B, H, T, hd = 2, 4, 96, 64
+    qkv = (torch.randn(3 * B * H * T * hd, device="cuda")).bfloat16()
+    x = torch.randn(B * T, H * hd, device="cuda")
+    gam, bet = torch.randn(H * hd, device="cuda"), torch.randn(H * hd, device="cuda")
+
+    def f(qkv, x):
+        out = torch.empty(B * T, H * hd, device="cuda", dtype=torch.bfloat16)
+        kw.attention(qkv, B, H, T, hd, out)
+        y = torch.empty_like(x)
+        kw.layernorm(x, gam, bet, 1e-5, y, None)
+        return out.float().sum() + y.sum(), out, y
+
+    eager = f(qkv, x.clone())
+    comp = torch.compile(f, fullgraph=True, backend="aot_eager")(qkv, x.clone())
+    for a, b in zip(eager, comp):
+        assert torch.equal(a, b)
