@@ -2,14 +2,15 @@
 """Headline benchmark: audio-seconds/sec of whisper-large-v3 greedy generate, 30 s clips, batch 32/GPU.
 
 One step = one batch of 32 synthetic 30 s clips resident in HBM -> log-mel (HIP) -> encoder ->
-cross-K/V -> greedy decode (4-token prompt, max_length 128 -> 128 new tokens, hipGraph step) on the
+greedy decode (cross-attention read from the encoder output: kw_cross_attn_enc) (4-token prompt, max_length 128 -> 128 new tokens, hipGraph step) on the
 MI355X engine (bf16).  Weights are random-init of the large-v3 architecture (no checkpoints offline).
 N > 1: one process per GPU (torchrun), each rank decodes its own batches (data parallel, weak
 scaling), token ids are all-gathered over RCCL at the end (run_pseudo_labelling.py:339-341), and the
 time is the max over ranks.
 
-Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` of the dominant kernel (cross-attention
-K/V streaming, HBM-bound), ``encoder_mfma`` (encoder MFMA fraction), ``cpu_baseline`` (reference
+Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` of the decode attention (the cross-attention's
+stream of the encoder output, HBM-bound), ``encoder_mfma`` (encoder MFMA fraction), ``decode_kernel_us``
+(per-launch device time of each decode-step kernel, in step context), ``cpu_baseline`` (reference
 transformers path on the host cores, bounded sample).
 """
 from __future__ import annotations
@@ -200,17 +201,51 @@ def main():
         return e0.elapsed_time(e1) / n * 1e-3
 
     H, S, hd = eng.H, shape.max_source_positions, 64
-    qx = sess._buffers(1)["qx"]
-    attn_out = sess._buffers(1)["attn"]
-    ws = sess._buffers(1)["ws"]
     n_dec = shape.decoder_layers
 
-    def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
-        for li in range(n_dec):
-            ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[2 * li], sess.cross[2 * li + 1], S, attn_out, ws)
+    def step_kernel_times(passes=3):
+        """Per-kernel device time inside the decode step: the step's launch sequence run eagerly with HIP
+        events around every launch (on the launch stream), so each kernel sees the cache state the graph
+        replay gives it (the other kernels' weight streams between two cross-attention launches)."""
+        seq = sess._step_plans(1)
+        tot, cnt = {}, {}
+        for _ in range(passes):
+            evs = []
+            for item in seq:
+                tag = item[0] if isinstance(item, tuple) else getattr(item, "tag", None) or "linear"
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                sess._run([item])
+                e1.record(stream)
+                evs.append((tag, e0, e1))
+            evs[-1][2].synchronize()
+            for tag, e0, e1 in evs:
+                tot[tag] = tot.get(tag, 0.0) + e0.elapsed_time(e1) * 1e3
+                cnt[tag] = cnt.get(tag, 0) + 1
+        return {k: round(tot[k] / cnt[k], 2) for k in tot}
 
-    cross_t = time_fn(cross_all_layers, max(1, iters // 4)) / n_dec
-    cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
+    kern_us = step_kernel_times()
+    if sess.use_enc:
+        # cross-attention over the encoder output: algorithmic bytes = the batch's encoder output, read once
+        # per launch (+ the queries u and the output z); one launch per decoder layer, all on the same e
+        cross_kernel = "xattn_enc_kernel"
+        cross_bytes = B * S * shape.d_model * 2 + 2 * B * H * shape.d_model * 2
+        cross_t = kern_us["xenc"] * 1e-6
+        cross_note = ("xattn_enc_kernel (decoder cross-attention over the encoder output, K/V projections absorbed; "
+                      "one launch per layer; rocprof name)")
+    else:
+        qx = sess._buffers(1)["qx"]
+        attn_out = sess._buffers(1)["attn"]
+        ws = sess._buffers(1)["ws"]
+
+        def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
+            for li in range(n_dec):
+                ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[2 * li], sess.cross[2 * li + 1], S, attn_out, ws)
+
+        cross_kernel = "cross_attn_kernel"
+        cross_t = time_fn(cross_all_layers, max(1, iters // 4)) / n_dec
+        cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
+        cross_note = "cross_attn_kernel (decoder cross-attention K/V stream, one launch per layer; rocprof name)"
     feats = fe.extract(audio)
     enc_t = time_fn(lambda: eng.encode(feats), 3)
     step_graph = sess._graph
@@ -235,15 +270,16 @@ def main():
                    "max_length": a.max_length, "new_tokens": new_tokens, "seq_len": 1500,
                    "pipelined": a.pipeline, "encoder_cus": a.encoder_cus if a.pipeline else None,
                    "parallelism": f"dp{world}"},
-        "roofline": {"kernel": "cross_attn_kernel (decoder cross-attention K/V stream, one launch per layer; rocprof name)",
+        "roofline": {"kernel": cross_note,
                      "bound": "hbm", "achieved": cross_bytes / cross_t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": cross_bytes / cross_t / 1e9 / HBM_PEAK_GBS, "traffic": None,
                      "bytes_per_launch": cross_bytes, "avg_launch_us": cross_t * 1e6},
         "encoder_mfma": {"ms": enc_t * 1e3, "tflops": ENC_FLOP_PER_CLIP * B / enc_t / 1e12,
                          "frac": ENC_FLOP_PER_CLIP * B / enc_t / 1e12 / BF16_PEAK_TFLOPS},
         "decode_step_ms": step_t * 1e3 if step_t else None,
+        "decode_kernel_us": kern_us,
     }
-    traffic, src = pmc_traffic("cross_attn_kernel")
+    traffic, src = pmc_traffic(cross_kernel)
     result["roofline"]["traffic"] = traffic
     result["roofline"]["traffic_source"] = src
     if rank == 0 and world == 1 and not a.no_cpu_baseline:

@@ -18,7 +18,7 @@ int kw_set_error_msg(int code, const char* msg) {
   return code;
 }
 
-extern "C" int kw_version(void) { return 102; }
+extern "C" int kw_version(void) { return 103; }
 
 extern "C" const char* kw_last_error(void) { return g_err; }
 

@@ -103,9 +103,11 @@ class KWhisperForConditionalGeneration:
         return _Encoder(self.engine)
 
     @classmethod
-    def from_state_dict(cls, shape, state_dict, *, dtype=torch.bfloat16, device="cuda", generation_config=None):
+    def from_state_dict(cls, shape, state_dict, *, dtype=torch.bfloat16, device="cuda", generation_config=None,
+                        cross_attention="kv_cache"):
         shape = PRESETS[shape] if isinstance(shape, str) else shape
-        return cls(WhisperEngine(shape, state_dict, dtype=dtype, device=device, generation_config=generation_config))
+        return cls(WhisperEngine(shape, state_dict, dtype=dtype, device=device, generation_config=generation_config,
+                                 cross_attention=cross_attention))
 
     @classmethod
     def from_pretrained(cls, path_or_name, *, torch_dtype=torch.bfloat16, device="cuda", **kw):

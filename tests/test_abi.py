@@ -39,7 +39,7 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_version(lib):
-    assert lib.kw_version() == 102
+    assert lib.kw_version() == 103
 
 
 def _c_layout(struct, fields):

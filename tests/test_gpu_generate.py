@@ -24,11 +24,12 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def _model(shape, dtype, pad=None):
+def _model(shape, dtype, pad=None, cross_attention="kv_cache"):
     from kwhisper.generation import KWhisperForConditionalGeneration
 
     return KWhisperForConditionalGeneration.from_state_dict(
-        shape, synthetic_state_dict(shape, 0), dtype=dtype, generation_config=generation_constants(shape, pad))
+        shape, synthetic_state_dict(shape, 0), dtype=dtype, generation_config=generation_constants(shape, pad),
+        cross_attention=cross_attention)
 
 
 @pytest.fixture(scope="module")
@@ -102,9 +103,14 @@ def test_tiny_fp32_logits(gold, tiny32):
     np.testing.assert_allclose(got, val, atol=1e-3, rtol=0)  # north-star: logits within 1e-3 fp32
 
 
-def test_tiny_bf16_logits_and_tokens(gold, tiny16):
+@pytest.mark.parametrize("cross", ["kv_cache", "encoder_output"])
+def test_tiny_bf16_logits_and_tokens(gold, tiny16, cross):
+    """bf16 tiny: teacher-forced logits and margin-gated greedy tokens (cross="encoder_output": the decode's
+    cross-attention over the encoder output, 4-position prefill as 24 queries in one launch)."""
     g = gold("tiny_fp32")
     feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    if cross != "kv_cache":
+        tiny16 = _model(TINY, torch.bfloat16, cross_attention=cross)
     eng = tiny16.engine
     sess = eng.new_session(feats.shape[0], eng.encode(feats))
     seq = torch.from_numpy(g["greedy_sequences"])
@@ -112,7 +118,7 @@ def test_tiny_bf16_logits_and_tokens(gold, tiny16):
     idx, val = g["greedy_logits_top_idx"], g["greedy_logits_top_val"]
     got = torch.gather(lg[:, : idx.shape[1]], -1, torch.from_numpy(idx.astype(np.int64))).numpy()
     err = np.abs(got - val)
-    print("tiny bf16 teacher-forced logit err: max %.4f mean %.4f" % (err.max(), err.mean()))
+    print("tiny bf16 (%s) teacher-forced logit err: max %.4f mean %.4f" % (cross, err.max(), err.mean()))
     assert err.max() < 0.25 and err.mean() < 0.03   # bf16 weights/activations, f32 accumulation
     toks = tiny16.generate(feats, language="ja", task="transcribe", max_length=128).cpu().numpy()
     want = g["greedy_tokens"]
@@ -140,9 +146,12 @@ def test_large_fp32_bitexact(gold, shape, tag):
     torch.cuda.empty_cache()
 
 
-def test_large_bf16_vs_reference(gold):
+@pytest.mark.parametrize("cross", ["kv_cache", "encoder_output"])
+def test_large_bf16_vs_reference(gold, cross):
+    """bf16 large-v3 against the fp32 HF fixture; cross="encoder_output" decodes with kw_cross_attn_enc (the
+    cross K/V projections absorbed into the query / value linears) under the same bars."""
     g = gold("large_v3_fp32")
-    model = _model(LARGE_V3, torch.bfloat16)
+    model = _model(LARGE_V3, torch.bfloat16, cross_attention=cross)
     feats = torch.from_numpy(oracle_features(LARGE_V3, g["cases"])).cuda()
     eng = model.engine
     enc = eng.encode(feats)
@@ -151,12 +160,13 @@ def test_large_bf16_vs_reference(gold):
     print("large-v3 bf16 encoder rel err", rel)
     assert rel < 0.05
     sess = eng.new_session(2, enc)
+    assert sess.use_enc == (cross == "encoder_output")
     seq = torch.from_numpy(g["greedy_sequences"])
     lg = sess.teacher_forced_logits(seq[:, :-1], 4).cpu()
     idx, val = g["greedy_logits_top_idx"], g["greedy_logits_top_val"]
     got = torch.gather(lg[:, : idx.shape[1]], -1, torch.from_numpy(idx.astype(np.int64))).numpy()
     err = np.abs(got - val)
-    print("large-v3 bf16 teacher-forced logit err: max %.4f mean %.4f" % (err.max(), err.mean()))
+    print("large-v3 bf16 (%s) teacher-forced logit err: max %.4f mean %.4f" % (cross, err.max(), err.mean()))
     assert err.max() < 0.35 and err.mean() < 0.03  # the same bars as config 3 at B = 32 (test_gpu_workloads.py)
     del model, sess
     torch.cuda.empty_cache()
