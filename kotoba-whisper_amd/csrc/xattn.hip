@@ -51,6 +51,7 @@ namespace {
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int v2u32;
+typedef __attribute__((ext_vector_type(4))) unsigned int v4u32;
 
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int NBUF = 3;      // ring slots per wave (2 sub-tiles in flight while one is consumed)
@@ -119,11 +120,11 @@ __device__ __forceinline__ void ds_wr16(char* p, uint32_t v) {
   asm volatile("ds_write_b16 %0, %1" ::"v"(lds_addr(p)), "v"(v) : "memory");
 }
 // write-through (agent-coherent) 16-B global accesses for the chunk partials
-__device__ __forceinline__ void st16_sc1(float* p, f32x4 v) {
+__device__ __forceinline__ void st16_sc1(void* p, v4u32 v) {
   asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
 }
-__device__ __forceinline__ f32x4 ld16_sc1(const float* p) {
-  f32x4 v;
+__device__ __forceinline__ v4u32 ld16_sc1(const void* p) {
+  v4u32 v;
   asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
   return v;
 }
@@ -132,6 +133,24 @@ __device__ __forceinline__ f32x4 ld16_sc1(const float* p) {
 template <int CTRL>
 __device__ __forceinline__ float dppf(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+// lane ^ 16 / lane ^ 32 exchanges by v_permlane16/32_swap (VALU; no LDS round trip like ds_bpermute): with
+// both operands = v, one result is the lane's own value and the other its partner's
+__device__ __forceinline__ float xor16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float xor16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 __device__ __forceinline__ float row16_max(float v) {
   v = fmaxf(v, dppf<0xB1>(v));
@@ -168,7 +187,7 @@ struct XaP {
   int q_len, qi0, Q;  // Q = rows * H queries per item in this launch (<= QMAX)
   int nch, nst;       // chunks per item, 16-frame sub-tiles per item
   float* ml;          // [B*nch][QMAX][2] chunk (max, sum)
-  float* zp;          // [B*nch][QMAX][D] chunk partial z (unnormalised)
+  bf16_t* zp;         // [B*nch][QMAX][D] chunk partial z (unnormalised, bf16: half the merge traffic)
   int* cnt;           // [B] arrivals   (zero before, left zero)
   int* dep;           // [B] departures (zero before, left zero)
   int* err;           // [1] set when an item barrier timed out
@@ -177,14 +196,15 @@ struct XaP {
 
 template <int NW, int KS>
 __global__ __launch_bounds__(NW * 64) void xattn_enc_kernel(XaP p) {
-  constexpr int CPW = 32 * KS;              // channels per wave
+  constexpr int CPW = 32 * KS;              // channels per wave (z phase)
   constexpr int WREG = KS * 1024;           // one wave's part of a ring slot
   constexpr int SLOT = NW * WREG;
+  constexpr int SB = NW * KS / 2;           // 32-channel blocks of a score wave (half the channels)
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  char* ring = lds;                                     // [NBUF][NW][KS][1 KB]
-  char* red = lds + NBUF * SLOT;                        // [NW][QMAX][16 frames] f32 partial scores
-  char* pimg = red + NW * QMAX * 16 * 4;                // [QMAX][16 frames] bf16 (32-B rows)
-  char* alph = pimg + QMAX * 32;                        // [QMAX] f32
+  char* ring = lds;                                        // [NBUF][NW][KS][1 KB]
+  char* red = lds + NBUF * SLOT;                           // [HB][64 lanes] f32x4: second-half partial scores
+  char* pimg = red + HB * 64 * 16;                         // [QMAX][16 frames] bf16 (32-B rows): P
+  char* alph = pimg + QMAX * 32;                           // [QMAX] f32 rescale factors, then [HB] int flags
   float* wts = reinterpret_cast<float*>(lds + p.wts_off);  // [NCHMAX][QMAX] combine weights
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -196,6 +216,9 @@ __global__ __launch_bounds__(NW * 64) void xattn_enc_kernel(XaP p) {
   const bf16_t* encb = p.enc + (int64_t)b * p.S * D;
   const int ch0 = wave * CPW;
   const int64_t qrow0 = ((int64_t)b * p.q_len + p.qi0) * p.H;  // first query's row in u / z
+  // score waves: wave w < 2 HB owns query block hb = w % HB over channel half w / HB
+  const bool swave = wave < 2 * HB;
+  const int shb = wave % HB, shalf = wave / HB;
 
   // sub-tile t of this chunk -> ring slot t % NBUF, this wave's channels: KS 1-KB LDS-DMA pieces, piece s =
   // 16 frames x 32 channels, lane i -> frame i>>2, 16-B chunk (i&3) ^ ((frame>>1)&3) of the block
@@ -209,143 +232,168 @@ __global__ __launch_bounds__(NW * 64) void xattn_enc_kernel(XaP p) {
     }
   };
 
-  f32x4 zacc[HB][2 * KS];
+  // z accumulators on v_mfma_f32_32x32x16_bf16: block k = channels ch0 + 32k; lane holds channel l&31,
+  // queries (r&3) + 8(r>>2) + 4(l>>5)
+  f32x16 zacc[KS];
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
+  for (int k = 0; k < KS; ++k)
 #pragma unroll
-    for (int cb = 0; cb < 2 * KS; ++cb) zacc[hb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // finalising lanes: query 4w + (l>>4) + 4*NW*pass, frame l&15 (NW = 4: two passes cover 32 queries)
-  constexpr int QP = QMAX / (4 * NW);
-  float m_run[QP], l_run[QP];
-#pragma unroll
-  for (int qp = 0; qp < QP; ++qp) {
-    m_run[qp] = -INFINITY;
-    l_run[qp] = 0.f;
-  }
+    for (int r = 0; r < 16; ++r) zacc[k][r] = 0.f;
+  // online softmax state (score waves of the first half): query fr + 16 shb, log2 domain, replicated in the
+  // query's 4 lanes; the reference max m_ref moves only when a sub-tile's max exceeds it by RESCALE_LOG2
+  // (rescaling z is then rare); p = exp2(s - m_ref) <= 2^RESCALE_LOG2
+  constexpr float RESCALE_LOG2 = 8.f;
+  float m_ref = -INFINITY, l_run = 0.f;
 
-  for (int i = tid; i < (QMAX * 32 + QMAX * 4) / 4; i += NW * 64) reinterpret_cast<float*>(pimg)[i] = 0.f;
-  __syncthreads();
   XSTAMP(0);
   issue(0);
-  if (nt > 1) issue(1);
-  // u fragments (loaded behind the first two sub-tiles; the compiler's wait for them before the loop
-  // drains those too, so the loop's counted vmcnt waits only ever see ring pieces)
-  // (B operand of S^T-partial = e_rows . u): lane holds u[query 16hb + (l&15)][ch0 + 32s + 8(l>>4) ..]
-  bf16x8 uf[HB][KS];
+  // u fragments of a score wave (B operand of S = e_rows . u): lane holds u[query 16 shb + (l&15)][32 sb + 8(l>>4) ..]
+  // for its half's blocks sb (loaded behind sub-tile 0; the compiler's wait for them drains it too, so the loop's
+  // counted vmcnt waits only ever see ring pieces)
+  bf16x8 uf[SB];
+  {
+    const int j = 16 * shb + (lane & 15);
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb) {
-    const int j = 16 * hb + (lane & 15);
-#pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      if (j < Q) {
-        uf[hb][s] = *reinterpret_cast<const bf16x8*>(p.u + (qrow0 + j) * D + ch0 + 32 * s + 8 * (lane >> 4));
+    for (int s = 0; s < SB; ++s) {
+      if (swave && j < Q) {
+        uf[s] = *reinterpret_cast<const bf16x8*>(p.u + (qrow0 + j) * D + 32 * (shalf * SB + s) + 8 * (lane >> 4));
       } else {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) uf[hb][s][e] = (__bf16)0.0f;
+        for (int e = 0; e < 8; ++e) uf[s][e] = (__bf16)0.0f;
       }
     }
   }
-
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
-#pragma unroll
-    for (int s = 0; s < KS; ++s) tie(uf[hb][s]);
+  for (int s = 0; s < SB; ++s) tie(uf[s]);
+  if (nt > 1) issue(1);  // (behind the compiler's wait for u and sub-tile 0: the loop starts on sub-tile 0 alone)
   const int fr = lane & 15, fg = lane >> 4;  // fragment row / 16-B group
   XSTAMP(1);
   for (int t = 0; t < nt; ++t) {
     if (t + 2 < nt) {
-      issue(t + 2);  // into slot (t-1) % NBUF: this wave's reads of it completed in step t-1
+      issue(t + 2);  // into slot (t-1) % NBUF: every wave's reads of it completed before barrier C of step t-1
       vmwait<2 * KS>();
     } else if (t + 1 < nt) {
       vmwait<KS>();
     } else {
       vmwait<0>();
     }
-    const char* sl = ring + (t % NBUF) * SLOT + wave * WREG;
+    const char* sl = ring + (t % NBUF) * SLOT;
     XSTAMP(8 + 8 * t);
+    raw_barrier();  // A: every wave's pieces of sub-tile t have landed
     if (KW_XENC_LAB == 2) continue;
-    // 1. partial scores over this wave's channels: S[frame][query]
-    bf16x8 a[KS];
+    // 1. score waves: S[frame 4fg + i][query fr + 16 shb] over their channel half (C layout = the z MFMA's
+    //    A-operand layout of P: query on the lane, 4 frames in the registers)
+    f32x4 sacc = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (swave) {
+      auto rd = [&](int s0, bf16x8 (&a)[KS]) {
 #pragma unroll
-    for (int s = 0; s < KS; ++s) a[s] = ds_rd128(sl + s * 1024 + fr * 64 + ((fg ^ ((fr >> 1) & 3)) << 4));
-    lgkm0();
+        for (int s = 0; s < KS; ++s) {
+          const int blk = shalf * SB + s0 + s;  // global 32-channel block -> owning wave's region
+          a[s] = ds_rd128(sl + (blk / KS) * WREG + (blk % KS) * 1024 + fr * 64 + ((fg ^ ((fr >> 1) & 3)) << 4));
+        }
+      };
+      bf16x8 a0[KS], a1[KS];
+      rd(0, a0);
 #pragma unroll
-    for (int s = 0; s < KS; ++s) tie(a[s]);
-    f32x4 sacc[HB];
+      for (int s0 = 0; s0 < SB; s0 += 2 * KS) {  // reads of the next KS blocks in flight beside the MFMAs
+        if (s0 + KS < SB) rd(s0 + KS, a1);
+        if (s0 + KS < SB) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(KS) : "memory");
+        else lgkm0();
 #pragma unroll
-    for (int hb = 0; hb < HB; ++hb) {
-      sacc[hb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < KS; ++s) tie(a0[s]);
 #pragma unroll
-      for (int s = 0; s < KS; ++s) sacc[hb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], uf[hb][s], sacc[hb], 0, 0, 0);
-      ds_wr128f_mfma(red + ((wave * QMAX + 16 * hb + fr) * 16 + 4 * fg) * 4, sacc[hb]);
-    }
-    lgkm0();
-    XSTAMP(9 + 8 * t);
-    raw_barrier();
-    XSTAMP(10 + 8 * t);
-    // 2. finalising lanes (query 4w + (l>>4) [+ 4 NW per pass], frame l&15): the NW partial scores summed in
-    //    wave order, online softmax with 16-lane DPP row reductions
+        for (int s = 0; s < KS; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[s], uf[s0 + s], sacc, 0, 0, 0);
+        if (s0 + KS >= SB) break;
+        if (s0 + 2 * KS < SB) rd(s0 + 2 * KS, a0);
+        if (s0 + 2 * KS < SB) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(KS) : "memory");
+        else lgkm0();
 #pragma unroll
-    for (int qp = 0; qp < QP; ++qp) {
-      if ((4 * NW * qp + 4 * wave) >= Q) continue;  // wave-uniform
-      const int j = 4 * NW * qp + 4 * wave + fg;
-      float pr[NW];
+        for (int s = 0; s < KS; ++s) tie(a1[s]);
 #pragma unroll
-      for (int w2 = 0; w2 < NW; ++w2) pr[w2] = ds_rd32f(red + ((w2 * QMAX + j) * 16 + fr) * 4);
+        for (int s = 0; s < KS; ++s) sacc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[s], uf[s0 + KS + s], sacc, 0, 0, 0);
+      }
+      if (shalf == 1) ds_wr128f_mfma(red + (shb * 64 + lane) * 16, sacc);
       lgkm0();
+    }
+    XSTAMP(9 + 8 * t);
+    raw_barrier();  // B: second-half partials published
+    XSTAMP(10 + 8 * t);
+    // 2. first-half score waves: full scores (halves summed in order), online softmax, P and the rescale factors
+    if (swave && shalf == 0) {
+      f32x4 other = ds_rd128f(red + (shb * 64 + lane) * 16);
+      lgkm0();
+      tie(other);
+      // (the MFMA result sacc is read by VALU here: the compiler inserts the wait states)
+      f32x4 sc = sacc + other;
+      const int f0 = (st0 + t) * SUB + 4 * fg;
+      float mt = -INFINITY;
 #pragma unroll
-      for (int w2 = 0; w2 < NW; ++w2) tie(pr[w2]);
-      float sc = pr[0];
+      for (int i = 0; i < 4; ++i) {
+        sc[i] = f0 + i < fend ? sc[i] * LOG2E : -INFINITY;
+        mt = fmaxf(mt, sc[i]);
+      }
+      mt = xor32_max(xor16_max(mt));
+      const bool bump = mt > m_ref + RESCALE_LOG2;  // (first sub-tile: m_ref = -inf)
+      const float al = bump ? __builtin_amdgcn_exp2f(m_ref - mt) : 1.f;
+      if (bump) {
+        l_run *= al;
+        m_ref = mt;
+      }
+      float pv[4];
 #pragma unroll
-      for (int w2 = 1; w2 < NW; ++w2) sc += pr[w2];
-      if ((st0 + t) * SUB + fr >= fend) sc = -INFINITY;
-      const float m_new = fmaxf(m_run[qp], row16_max(sc));  // finite: every sub-tile holds a valid frame
-      const float al = __builtin_amdgcn_exp2f((m_run[qp] - m_new) * LOG2E);  // 0 on the first sub-tile
-      const float pv = __builtin_amdgcn_exp2f(fmaf(sc, LOG2E, -m_new * LOG2E));
-      l_run[qp] = fmaf(al, l_run[qp], row16_sum(pv));
-      m_run[qp] = m_new;
-      ds_wr16(pimg + j * 32 + fr * 2, pack_bf16x2(pv, 0.f));
-      if (fr == 0) ds_wr32f(alph + j * 4, al);
+      for (int i = 0; i < 4; ++i) pv[i] = __builtin_amdgcn_exp2f(sc[i] - m_ref);
+      l_run += xor32_sum(xor16_sum((pv[0] + pv[1]) + (pv[2] + pv[3])));
+      ds_wr64(pimg + (16 * shb + fr) * 32 + 8 * fg, v2u32{pack_bf16x2(pv[0], pv[1]), pack_bf16x2(pv[2], pv[3])});
+      if (fg == 0) ds_wr32f(alph + (16 * shb + fr) * 4, al);
+      const int anyb = (__builtin_amdgcn_read_exec() & __ballot(bump)) != 0;
+      if (lane == 0) ds_wr32f(alph + QMAX * 4 + shb * 4, __int_as_float(anyb));
       lgkm0();
     }
     XSTAMP(11 + 8 * t);
-    raw_barrier();
+    raw_barrier();  // C: P and the rescale factors published
     XSTAMP(12 + 8 * t);
-    // 3. z = alpha z + P e over this wave's channels: A = P [query][frame], B = e [frame][channel] (transposed
-    //    reads: group g = l>>4 takes frames 4g..4g+3, lane 4q+p of the group addresses frame 4g+q,
-    //    channels 4p..4p+3 of the 16-channel block)
-    f32x4 av[HB];
-    v2u32 pa[HB];
+    // 3. z = alpha z + P e over this wave's channels on v_mfma_f32_32x32x16_bf16: A = P [query l&31][frames
+    //    8(l>>5) ..], B = e [frames 8(l>>5) ..][channel l&31] by two transposed reads of this wave's own pieces
+    //    (group g = l>>4: frames 8hh + 4j' + q for lane 4q+p, channels 16(g&1) + 4p .. of the 32-channel block)
+    bf16x8 pa = ds_rd128(pimg + (lane & 31) * 32 + 16 * (lane >> 5));
+    int rescale = 0;
 #pragma unroll
-    for (int hb = 0; hb < HB; ++hb) {
-      av[hb] = ds_rd128f(alph + (16 * hb + 4 * fg) * 4);
-      pa[hb] = ds_rd64(pimg + (fr + 16 * hb) * 32 + 8 * fg);
-    }
-    v2u32 bt[2 * KS];
+    for (int hb = 0; hb < HB; ++hb) rescale |= __float_as_int(ds_rd32f(alph + QMAX * 4 + hb * 4));
+    v2u32 bt[KS][2];
     {
-      const int trow = 4 * fg + ((lane & 15) >> 2), pp = lane & 3;
+      const char* own = sl + wave * WREG;
+      const int hh = lane >> 5, g = (lane >> 4) & 1, q = (lane & 15) >> 2, pp = lane & 3;
+      const int cc = 2 * g + (pp >> 1);
 #pragma unroll
-      for (int cb = 0; cb < 2 * KS; ++cb) {
-        const int cc = 2 * (cb & 1) + (pp >> 1);
-        bt[cb] = ds_tr64(sl + (cb >> 1) * 1024 + trow * 64 + ((cc ^ ((trow >> 1) & 3)) << 4) + 8 * (pp & 1));
-      }
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int r = 8 * hh + 4 * h2 + q;
+          bt[k][h2] = ds_tr64(own + k * 1024 + r * 64 + ((cc ^ ((r >> 1) & 3)) << 4) + 8 * (pp & 1));
+        }
     }
     lgkm0();
+    tie(pa);
+    tie(rescale);
 #pragma unroll
-    for (int hb = 0; hb < HB; ++hb) {
-      tie(av[hb]);
-      tie(pa[hb]);
+    for (int k = 0; k < KS; ++k) {
+      tie(bt[k][0]);
+      tie(bt[k][1]);
+    }
+    if (__builtin_amdgcn_readfirstlane(rescale)) {  // wave-uniform, rare after the first sub-tile
+      f32x4 av[4];
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) av[g4] = *reinterpret_cast<const f32x4*>(alph + (8 * g4 + 4 * (lane >> 5)) * 4);
+#pragma unroll
+      for (int k = 0; k < KS; ++k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) zacc[k][r] *= av[r >> 2][r & 3];
     }
 #pragma unroll
-    for (int cb = 0; cb < 2 * KS; ++cb) tie(bt[cb]);
-#pragma unroll
-    for (int hb = 0; hb < HB; ++hb)
-#pragma unroll
-      for (int cb = 0; cb < 2 * KS; ++cb) {
-        zacc[hb][cb] *= av[hb];
-        zacc[hb][cb] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, pa[hb]),
-                                                                 __builtin_bit_cast(s16x4, bt[cb]), zacc[hb][cb], 0, 0, 0);
-      }
+    for (int k = 0; k < KS; ++k) {
+      const v4u32 w = {bt[k][0][0], bt[k][0][1], bt[k][1][0], bt[k][1][1]};
+      zacc[k] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pa, __builtin_bit_cast(bf16x8, w), zacc[k], 0, 0, 0);
+    }
     XSTAMP(13 + 8 * t);
   }
   XSTAMP(2);
@@ -355,28 +403,24 @@ __global__ __launch_bounds__(NW * 64) void xattn_enc_kernel(XaP p) {
   __syncthreads();
   float* zt = reinterpret_cast<float*>(lds);  // [Q][D]
 #pragma unroll
-  for (int hb = 0; hb < HB; ++hb)
+  for (int k = 0; k < KS; ++k)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int j = 16 * hb + 4 * fg + i;
-      if (j < Q) {
-#pragma unroll
-        for (int cb = 0; cb < 2 * KS; ++cb) zt[j * D + ch0 + 16 * cb + fr] = zacc[hb][cb][i];
-      }
+    for (int r = 0; r < 16; ++r) {
+      const int j = (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+      if (j < Q) zt[j * D + ch0 + 32 * k + (lane & 31)] = zacc[k][r];
     }
   __syncthreads();
-  float* zpb = p.zp + (int64_t)blockIdx.x * QMAX * D;
+  bf16_t* zpb = p.zp + (int64_t)blockIdx.x * QMAX * D;
   if (KW_XENC_LAB != 1)
-    for (int idx = tid; idx < Q * (D >> 2); idx += NW * 64)
-      st16_sc1(zpb + 4 * idx, reinterpret_cast<const f32x4*>(zt)[idx]);
-#pragma unroll
-  for (int qp = 0; qp < QP; ++qp) {
-    const int j = 4 * NW * qp + 4 * wave + fg;
-    if (fr == 0 && j < Q) {
-      float* mlj = p.ml + ((int64_t)blockIdx.x * QMAX + j) * 2;
-      __hip_atomic_store(mlj, m_run[qp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(mlj + 1, l_run[qp], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int idx = tid; idx < Q * (D >> 3); idx += NW * 64) {  // 8 channels (16 B of bf16) per store
+      const f32x4 lo = reinterpret_cast<const f32x4*>(zt)[2 * idx], hi = reinterpret_cast<const f32x4*>(zt)[2 * idx + 1];
+      st16_sc1(zpb + 8 * idx, v4u32{pack_bf16x2(lo[0], lo[1]), pack_bf16x2(lo[2], lo[3]), pack_bf16x2(hi[0], hi[1]),
+                                    pack_bf16x2(hi[2], hi[3])});
     }
+  if (swave && shalf == 0 && fg == 0 && 16 * shb + fr < Q) {  // the softmax state of query 16 shb + fr
+    float* mlj = p.ml + ((int64_t)blockIdx.x * QMAX + 16 * shb + fr) * 2;
+    __hip_atomic_store(mlj, m_ref, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(mlj + 1, l_run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   XSTAMP(3);
@@ -400,7 +444,7 @@ __global__ __launch_bounds__(NW * 64) void xattn_enc_kernel(XaP p) {
   }
   XSTAMP(5);
   // 6. merge: this workgroup finalises channels [D c / nch, D (c+1) / nch) of every query, chunks in order
-  const int cb0 = 4 * (((D >> 2) * c) / p.nch), cb1 = 4 * (((D >> 2) * (c + 1)) / p.nch);  // whole float4 groups
+  const int cb0 = 8 * (((D >> 3) * c) / p.nch), cb1 = 8 * (((D >> 3) * (c + 1)) / p.nch);  // whole 8-channel groups
   const float* mlb = p.ml + (int64_t)b * p.nch * QMAX * 2;
   if (tid < Q) {
     float mk[NCHMAX], M = -INFINITY;
@@ -412,7 +456,7 @@ __global__ __launch_bounds__(NW * 64) void xattn_enc_kernel(XaP p) {
     float L = 0.f, f[NCHMAX];
 #pragma unroll
     for (int k = 0; k < NCHMAX; ++k) {
-      f[k] = k < p.nch ? __builtin_amdgcn_exp2f((mk[k] - M) * LOG2E) : 0.f;
+      f[k] = k < p.nch ? __builtin_amdgcn_exp2f(mk[k] - M) : 0.f;  // (chunk maxima in the log2 domain)
       if (k < p.nch)
         L = fmaf(__hip_atomic_load(mlb + (k * QMAX + tid) * 2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), f[k], L);
     }
@@ -421,17 +465,17 @@ __global__ __launch_bounds__(NW * 64) void xattn_enc_kernel(XaP p) {
     for (int k = 0; k < NCHMAX; ++k) wts[k * QMAX + tid] = f[k] * inv;
   }
   __syncthreads();
-  const int cw4 = (cb1 - cb0) >> 2;
-  const float* zpi = p.zp + (int64_t)b * p.nch * QMAX * D;
-  const int nit = KW_XENC_LAB == 1 ? 0 : Q * cw4;
-  for (int idx0 = tid; idx0 < nit; idx0 += 2 * NW * 64) {  // two 4-channel pieces per thread in flight
-    f32x4 v[2][NCHMAX];
+  const int cw8 = (cb1 - cb0) >> 3;
+  const bf16_t* zpi = p.zp + (int64_t)b * p.nch * QMAX * D;
+  const int nit = KW_XENC_LAB == 1 ? 0 : Q * cw8;
+  for (int idx0 = tid; idx0 < nit; idx0 += 2 * NW * 64) {  // two 8-channel pieces per thread in flight
+    v4u32 v[2][NCHMAX];
     int jj[2], cc[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
       const int idx = min(idx0 + r * NW * 64, nit - 1);
-      jj[r] = idx / cw4;
-      cc[r] = cb0 + 4 * (idx - jj[r] * cw4);
+      jj[r] = idx / cw8;
+      cc[r] = cb0 + 8 * (idx - jj[r] * cw8);
 #pragma unroll
       for (int k = 0; k < NCHMAX; ++k) v[r][k] = ld16_sc1(zpi + ((int64_t)min(k, p.nch - 1) * QMAX + jj[r]) * D + cc[r]);
     }
@@ -441,15 +485,19 @@ __global__ __launch_bounds__(NW * 64) void xattn_enc_kernel(XaP p) {
 #pragma unroll
       for (int k = 0; k < NCHMAX; ++k) tie(v[r][k]);
       if (idx0 + r * NW * 64 >= nit) continue;
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < NCHMAX; ++k) {
         const float w = k < p.nch ? wts[k * QMAX + jj[r]] : 0.f;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[e] = fmaf(v[r][k][e], w, acc[e]);
+        for (int e = 0; e < 4; ++e) {
+          acc[2 * e] = fmaf(__uint_as_float(v[r][k][e] << 16), w, acc[2 * e]);
+          acc[2 * e + 1] = fmaf(__uint_as_float(v[r][k][e] & 0xffff0000u), w, acc[2 * e + 1]);
+        }
       }
-      const uint2 pk = make_uint2(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]));
-      *reinterpret_cast<uint2*>(p.z + (qrow0 + jj[r]) * D + cc[r]) = pk;
+      *reinterpret_cast<uint4*>(p.z + (qrow0 + jj[r]) * D + cc[r]) =
+          make_uint4(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
+                     pack_bf16x2(acc[6], acc[7]));
     }
   }
   XSTAMP(6);
@@ -491,7 +539,7 @@ constexpr int LDS_MAX = 160 * 1024;
 // Q query rows if larger, then the merge weights; sets p.wts_off
 template <int NW, int KS>
 size_t lds_bytes(XaP& p) {
-  const size_t loop = (size_t)NBUF * NW * KS * 1024 + NW * QMAX * 16 * 4 + QMAX * 32 + QMAX * 4;
+  const size_t loop = (size_t)NBUF * NW * KS * 1024 + HB * 64 * 16 + QMAX * 32 + QMAX * 4 + HB * 4;
   const size_t zt = (size_t)p.Q * p.D * 4;
   p.wts_off = (int)(((loop > zt ? loop : zt) + 15) / 16 * 16);
   return (size_t)p.wts_off + NCHMAX * QMAX * 4;
@@ -523,7 +571,7 @@ extern "C" int kw_lab_xenc_stamps(unsigned long long* host) {
 extern "C" size_t kw_cross_attn_enc_workspace(int64_t B, int64_t D) {
   if (B <= 0 || D <= 0) return 0;
   const int64_t blocks = B * chunks_for(B);
-  return hdr_bytes(B) + (size_t)blocks * QMAX * 2 * sizeof(float) + (size_t)blocks * QMAX * D * sizeof(float);
+  return hdr_bytes(B) + (size_t)blocks * QMAX * 2 * sizeof(float) + (size_t)blocks * QMAX * D * sizeof(bf16_t);
 }
 
 extern "C" int kw_cross_attn_enc(const void* enc, int64_t B, int64_t S, int64_t D, const void* u, int64_t q_len,
@@ -551,7 +599,7 @@ extern "C" int kw_cross_attn_enc(const void* enc, int64_t B, int64_t S, int64_t 
   p.dep = hdr + B;
   p.err = hdr + 2 * B;
   p.ml = (float*)((char*)workspace + hdr_bytes(B));
-  p.zp = p.ml + (size_t)B * chunks_for(B) * QMAX * 2;
+  p.zp = reinterpret_cast<bf16_t*>(p.ml + (size_t)B * chunks_for(B) * QMAX * 2);
   const int grid = (int)(B * p.nch);
   const int rows = QMAX / (int)H;  // decode rows per launch (one K/V-free pass over e serves them all)
   hipStream_t s = (hipStream_t)stream;

@@ -80,3 +80,32 @@ bench("B=32 one graph", gf.replay)
 bench("B=16 one half", ga.replay)
 bench("two halves, one stream", both_serial)
 bench("two halves, two streams (concurrent)", both_concurrent)
+
+# CU-masked streams: each half on its own half of the chip (kw_stream_create_cu_range)
+from kwhisper import ops  # noqa: E402
+
+ncu = torch.cuda.get_device_properties(0).multi_processor_count
+for split in (ncu // 2, (ncu * 5) // 8):
+    ma, mb = ops.cu_range_stream(0, split), ops.cu_range_stream(split, ncu)
+    gma = capture(lambda: ha._run(ha._step_plans(1)), ma)
+    gmb = capture(lambda: hb._run(hb._step_plans(1)), mb)
+    torch.cuda.synchronize()
+
+    def masked():
+        ma.wait_stream(cur)
+        mb.wait_stream(cur)
+        with torch.cuda.stream(ma):
+            gma.replay()
+        with torch.cuda.stream(mb):
+            gmb.replay()
+        cur.wait_stream(ma)
+        cur.wait_stream(mb)
+
+    def masked_a():
+        ma.wait_stream(cur)
+        with torch.cuda.stream(ma):
+            gma.replay()
+        cur.wait_stream(ma)
+
+    bench(f"B=16 half alone on CUs [0,{split})", masked_a)
+    bench(f"two halves, CU-masked {split}/{ncu - split}", masked)
