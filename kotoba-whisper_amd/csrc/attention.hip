@@ -333,9 +333,7 @@ __device__ __forceinline__ void attend_rows(const float qv[8], int k0, int k1, K
       float s = 0.f;
 #pragma unroll
       for (int i = 0; i < 8; ++i) s = fmaf(qv[i], kv[j][i], s);
-      s += __shfl_xor(s, 1, 64);
-      s += __shfl_xor(s, 2, 64);
-      s += __shfl_xor(s, 4, 64);
+      s = kw_sum8(s);
       const int k = kb + 32 * j;
       if (k < k1) {
         if (sub == 0) sc[k - k0] = s;
@@ -432,9 +430,7 @@ __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, 
     float sj = 0.f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kv[i], sj);
-    sj += __shfl_xor(sj, 1, 64);
-    sj += __shfl_xor(sj, 2, 64);
-    sj += __shfl_xor(sj, 4, 64);
+    sj = kw_sum8(sj);
     sc[j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
     mx = fmaxf(mx, sc[j]);
   }
@@ -455,9 +451,7 @@ __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, 
   // lanes of one wave with equal sub hold the same dims: reduce over lane bits 3..5
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    acc[i] += __shfl_xor(acc[i], 8, 64);
-    acc[i] += __shfl_xor(acc[i], 16, 64);
-    acc[i] += __shfl_xor(acc[i], 32, 64);
+    acc[i] = kw_sum_hi(acc[i]);
   }
   lsum = wave_sum(lsum) * 0.125f;  // every row's p was counted by its 8 lanes (exact: power of two)
   if (lane < 8) {
@@ -646,9 +640,7 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
         float sj = 0.f;
 #pragma unroll
         for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kv[i], sj);
-        sj += __shfl_xor(sj, 1, 64);
-        sj += __shfl_xor(sj, 2, 64);
-        sj += __shfl_xor(sj, 4, 64);
+        sj = kw_sum8(sj);
         sc[r][j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
         mx = fmaxf(mx, sc[r][j]);
       }
@@ -673,9 +665,7 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
       }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        acc[i] += __shfl_xor(acc[i], 8, 64);
-        acc[i] += __shfl_xor(acc[i], 16, 64);
-        acc[i] += __shfl_xor(acc[i], 32, 64);
+        acc[i] = kw_sum_hi(acc[i]);
       }
       lsum = wave_sum(lsum) * 0.125f;
       if (lane < 8) {

@@ -56,15 +56,55 @@ __device__ __forceinline__ float gelu_bf16out(float x) {
   return fmaf(fabsf(h), e, h);
 }
 
+// Cross-lane reductions on the VALU (DPP within 16-lane rows, v_permlane16/32_swap across them) instead of
+// ds_bpermute round trips through the LDS unit.  Every step combines a lane with exactly the partner of the
+// xor butterfly it replaces (quad_perm [1,0,3,2] = ^1, [2,3,0,1] = ^2; once 4- / 8-lane groups are uniform,
+// row_half_mirror / row_mirror pair them like ^4 / ^8; row_ror:8 = ^8; the swaps = ^16 / ^32) and + / max
+// are commutative, so results are bitwise those of the __shfl_xor butterflies they replace (max in any order).
+// The lanes a step reads must be active.
+template <int CTRL>
+__device__ __forceinline__ float kw_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float kw_swap16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float kw_swap32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float kw_swap16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float kw_swap32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+// sum over each aligned 8-lane group (lane bits 0..2): the ^1, ^2, ^4 butterfly
+__device__ __forceinline__ float kw_sum8(float v) {
+  v += kw_dpp<0xB1>(v);
+  v += kw_dpp<0x4E>(v);
+  return v + kw_dpp<0x141>(v);
+}
+// sum over lane bits 3..5 (lanes with equal l & 7): the ^8, ^16, ^32 butterfly
+__device__ __forceinline__ float kw_sum_hi(float v) {
+  v += kw_dpp<0x128>(v);
+  return kw_swap32_sum(kw_swap16_sum(v));
+}
+// (keeps the ^32 .. ^1 order of the original butterfly: a different association tree would change f32 sums)
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmaxf(v, kw_dpp<0xB1>(v));
+  v = fmaxf(v, kw_dpp<0x4E>(v));
+  v = fmaxf(v, kw_dpp<0x141>(v));
+  v = fmaxf(v, kw_dpp<0x140>(v));
+  return kw_swap32_max(kw_swap16_max(v));
 }
 
 #define KW_CHECK_LAUNCH()                                   \
