@@ -417,10 +417,18 @@ __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
   Row8<T> kr[8], vr[8];
+  // key groups j past the chunk (k0 + 32j >= k1: workgroup-uniform, e.g. the short self-attention chunks of
+  // early decode steps) load nothing and hold zeros (their scores are masked, p = 0)
 #pragma unroll
-  for (int j = 0; j < 8; ++j) kr[j] = ld_row8<T>(kp(min(k0 + slot + 32 * j, k1 - 1)) + sub * 8);
+  for (int j = 0; j < 8; ++j) {
+    if (k0 + 32 * j < k1) kr[j] = ld_row8<T>(kp(min(k0 + slot + 32 * j, k1 - 1)) + sub * 8);
+    else kr[j] = Row8<T>{};
+  }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) vr[j] = ld_row8<T>(vp(min(k0 + slot + 32 * j, k1 - 1)) + sub * 8);
+  for (int j = 0; j < 8; ++j) {
+    if (k0 + 32 * j < k1) vr[j] = ld_row8<T>(vp(min(k0 + slot + 32 * j, k1 - 1)) + sub * 8);
+    else vr[j] = Row8<T>{};
+  }
   float sc[8];
   float mx = -INFINITY;
 #pragma unroll
