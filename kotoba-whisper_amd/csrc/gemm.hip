@@ -421,6 +421,52 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
       const int bb = m / rpb;
       return (int64_t)bb * bstride + (int64_t)(m - bb * rpb) * rstride + coff;
     };
+    if constexpr (EPI == KW_EPI_RESID) {
+      // Residual add C(f32) += acc + bias: the C reads of 16-row block i+1 are issued before block i's
+      // staging, adds and stores, so each block waits on loads already in flight instead of one dependent
+      // round trip per row piece (28 -> 16 us per 256x256 tile at 48000 x 1280; a deeper ring spills).
+      constexpr int NP = 2 * (8 / RPI);  // row pieces per lane per 16-row block
+      f32x4 res[2][NP];
+      int64_t roff[2][NP];
+      auto issue = [&](int i, f32x4* r, int64_t* o) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+          for (int q = 0; q < 8 / RPI; ++q) {
+            const int lr = RPI * q + ln / LPR;
+            const int m = tm0 + grp * 128 + 16 * i + 4 * (lr >> 1) + 2 * hh + (lr & 1);
+            const int pi = hh * (8 / RPI) + q;
+            o[pi] = row_offset(min(m, p.M - 1));
+            r[pi] = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(p.C) + o[pi]);
+          }
+      };
+      issue(0, res[0], roff[0]);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if (i + 1 < 8) issue(i + 1, res[(i + 1) & 1], roff[(i + 1) & 1]);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r2 = 0; r2 < 2; ++r2)
+              ep[(2 * (ln >> 4) + r2) * P_EROW + 16 * j + (ln & 15)] = acc[i][j][2 * hh + r2];
+#pragma unroll
+          for (int q = 0; q < 8 / RPI; ++q) {
+            const int lr = RPI * q + ln / LPR;
+            const int m = tm0 + grp * 128 + 16 * i + 4 * (lr >> 1) + 2 * hh + (lr & 1);
+            const int pi = hh * (8 / RPI) + q;
+            f32x4 v4;
+            lds_issue_read(ep + lr * P_EROW + VEC * cq, v4);
+            lds_wait(v4);
+            if (m >= p.M) continue;
+            const f32x4 o = res[i & 1][pi];
+            *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.C) + roff[i & 1][pi]) =
+                f32x4{o[0] + (v4[0] + cb[0]), o[1] + (v4[1] + cb[1]), o[2] + (v4[2] + cb[2]), o[3] + (v4[3] + cb[3])};
+          }
+        }
+      }
+    } else
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
 #pragma unroll

@@ -133,6 +133,8 @@ def test_gemm256_persistent(M, K, bias):
     ra = torch.randn(7, N, device="cuda")
     ops.GemmPlan(A, W, C, M, N, K, bias=b, row_add=ra, row_add_period=7)()
     torch.testing.assert_close(C, ref + ra[torch.arange(M, device="cuda") % 7], atol=1e-3, rtol=1e-3)
+    ops.GemmPlan(A, W, Cb, M, N, K, bias=b, row_add=ra, row_add_period=7)()  # bf16 + row_add (the conv2 stem)
+    torch.testing.assert_close(Cb.float(), ref + ra[torch.arange(M, device="cuda") % 7], atol=2e-2, rtol=1e-2)
     H0 = torch.randn(M, N, device="cuda")
     Hc = H0.clone()
     ops.GemmPlan(A, W, Hc, M, N, K, bias=b, epilogue=L.KW_EPI_RESID)()

@@ -30,10 +30,15 @@ static void fill(unsigned short* d, size_t n, unsigned seed) {
 
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 48000, N = argc > 2 ? atoi(argv[2]) : 1280, K = argc > 3 ? atoi(argv[3]) : 1280;
+  const int mode = argc > 4 ? atoi(argv[4]) : 0;  // 0 store bf16, 1 bias+GELU bf16, 2 residual add into f32
   unsigned short *A, *W, *C;
+  float* bias;
   hipMalloc(&A, (size_t)M * K * 2);
   hipMalloc(&W, (size_t)N * K * 2);
-  hipMalloc(&C, (size_t)M * N * 2);
+  hipMalloc(&C, (size_t)M * N * 4);
+  hipMalloc(&bias, (size_t)N * 4);
+  hipMemset(bias, 0, (size_t)N * 4);
+  hipMemset(C, 0, (size_t)M * N * 4);
   fill(A, (size_t)M * K, 1);
   fill(W, (size_t)N * K, 2);
   unsigned long long* st;
@@ -44,6 +49,8 @@ int main(int argc, char** argv) {
   kw_gemm_args a = {};
   a.dtype = KW_DT_BF16; a.c_dtype = KW_DT_BF16; a.A = A; a.lda = K; a.W = W; a.C = C; a.ldc = N;
   a.M = M; a.N = N; a.K = K; a.epilogue = KW_EPI_STORE; a.scale = 1.f;
+  if (mode == 1) { a.gelu = 1; a.bias = bias; }
+  if (mode == 2) { a.epilogue = KW_EPI_RESID; a.c_dtype = KW_DT_F32; a.bias = bias; }
   for (int i = 0; i < 20; ++i) kw_gemm(&a, 0);
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
@@ -76,6 +83,7 @@ int main(int argc, char** argv) {
       if (t + 1 < 20 && nx) { s_gap += (nx - a3) / 100.0; ++n_gap; }
     }
   }
+  printf("mode %d ", mode);
   printf("M=%d N=%d K=%d  event %.1f us  stamped span %.1f us  WGs %d  last WG start %.2f us  first-main max %.2f us\n",
          M, N, K, ms * 1e3, (tend - t0) / 100.0, n_wg, start_max, first_main_max);
   printf("avg: entry->main %.2f us | main loop %.2f us | epilogue %.2f us | epilogue->next main %.2f us | tiles %d\n",
