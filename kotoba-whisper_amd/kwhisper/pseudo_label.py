@@ -10,10 +10,17 @@ dropped).  The only collectives are the per-batch width ``all_reduce(MAX)`` and 
 int64 ids (~1 KB/clip), over RCCL (``nccl``) on the GPU box or ``gloo`` on the CPU.
 
 The gathered predictions come back in dataset order, identical to a single-process run.
+
+Resume (SURVEY.md §5 checkpoint / resume: "skip shards whose output exists"): with ``checkpoint_dir`` every
+gathered round is written there by rank 0 as ``round_<step>.npz`` (numpy, no pickle; written to a temporary
+name and renamed, so a crash leaves whole files only).  A restarted run decodes only the rounds without a
+file -- rank 0's view of the directory is broadcast so every rank skips the same rounds and the
+collectives stay matched -- and reads the others back (one node: the directory is visible to every rank).
 """
 from __future__ import annotations
 
 import csv
+import os
 from typing import Callable, Iterable, List, Optional, Sequence
 
 import numpy as np
@@ -121,22 +128,95 @@ def _with_prompt(ids: torch.Tensor, prompt: Sequence[int]) -> torch.Tensor:
     return torch.cat([pre, ids], 1)
 
 
-def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode):
+def _round_path(checkpoint_dir: str, si: int) -> str:
+    return os.path.join(checkpoint_dir, f"round_{si:06d}.npz")
+
+
+def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict) -> List[bool]:
+    """Which gathered rounds already have a checkpoint file, as rank 0 sees it (broadcast: every rank skips
+    the same rounds, so the per-round collectives stay matched).  The directory's ``plan.json`` (items,
+    batch size, world size) must match this run's: the rounds of another plan hold other items."""
+    if not checkpoint_dir or n_steps == 0:
+        return [False] * n_steps
+    import json
+
+    dist = _dist()
+    rank = dist.get_rank() if dist else 0
+    mask = torch.zeros((n_steps + 1,), dtype=torch.int64, device=device)  # [0]: 1 = plan mismatch
+    if rank == 0:
+        meta = os.path.join(checkpoint_dir, "plan.json")
+        if os.path.exists(meta):
+            with open(meta) as f:
+                mask[0] = int(json.load(f) != plan)
+        else:
+            with open(meta + ".tmp", "w") as f:
+                json.dump(plan, f)
+            os.replace(meta + ".tmp", meta)
+        if not int(mask[0]):
+            for si in range(n_steps):
+                mask[si + 1] = int(os.path.exists(_round_path(checkpoint_dir, si)))
+    if dist is not None and dist.get_world_size() > 1:
+        dist.broadcast(mask, 0)
+    m = mask.cpu().tolist()
+    if m[0]:
+        raise ValueError(f"checkpoint_dir {checkpoint_dir} holds rounds of another plan than {plan} (plan.json)")
+    return [bool(x) for x in m[1:]]
+
+
+def _save_round(checkpoint_dir: str, si: int, fid: List[int], mats: List[np.ndarray]) -> None:
+    path = _round_path(checkpoint_dir, si)
+    tmp = f"{path}.{os.getpid()}.tmp"
+    with open(tmp, "wb") as f:
+        np.savez(f, fid=np.asarray(fid, dtype=np.int64), **{f"c{c}": m for c, m in enumerate(mats)})
+    os.replace(tmp, path)  # atomic: a restart sees the whole round or none of it
+
+
+def _load_round(checkpoint_dir: str, si: int):
+    with np.load(_round_path(checkpoint_dir, si), allow_pickle=False) as z:
+        n_cols = sum(1 for k in z.files if k.startswith("c"))
+        return z["fid"].tolist(), [z[f"c{c}"] for c in range(n_cols)]
+
+
+def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
+                checkpoint_dir=None):
     """Shared DP loop: ``decode(feats)`` -> list of id matrices (one per output column); each is padded
-    across ranks and gathered with the file ids (``run_pseudo_labelling.py:336-344``, v3 ``:309-321``)."""
+    across ranks and gathered with the file ids (``run_pseudo_labelling.py:336-344``, v3 ``:309-321``).
+    With ``checkpoint_dir``, gathered rounds are checkpointed and rounds already on disk are skipped."""
     dist = _dist()
     world = dist.get_world_size() if dist else 1
     rank = dist.get_rank() if dist else 0
     steps = shard_batches(n_items, batch_size, world, rank)
     rem = gather_remainder(n_items, batch_size, world)
+    if checkpoint_dir and rank == 0:
+        os.makedirs(checkpoint_dir, exist_ok=True)
+    mask_dev = comm_device if comm_device is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if dist is not None and dist.get_backend() == "nccl"
+        else torch.device("cpu"))
+    done = _done_rounds(checkpoint_dir, len(steps), mask_dev,
+                        {"n_items": int(n_items), "batch_size": int(batch_size), "world_size": int(world)})
     eval_ids: List[int] = []
     cols: Optional[List[List[np.ndarray]]] = None
     for si, idx in enumerate(steps):
+        if done[si]:  # decoded by an earlier run: read the gathered round back
+            fid_l, mats = _load_round(checkpoint_dir, si)
+            if cols is None:
+                cols = [[] for _ in mats]
+            if len(mats) != len(cols):
+                raise ValueError(f"checkpoint {_round_path(checkpoint_dir, si)} holds {len(mats)} output columns, "
+                                 f"this run produces {len(cols)}")
+            eval_ids.extend(fid_l)
+            for c, m in enumerate(mats):
+                cols[c].extend(m)
+            if on_step is not None:
+                on_step(si, len(steps))
+            continue
         outs = decode(features(idx))
         if cols is None:
             cols = [[] for _ in outs]
         last = si == len(steps) - 1 and rem > 0
         fid = None
+        round_fid: List[int] = []
+        round_mats: List[np.ndarray] = []
         for c, ids in enumerate(outs):
             ids = ids.to(comm_device) if comm_device is not None else ids
             ids = _all_gather_rows(pad_across_processes(ids, pad_token_id))
@@ -144,10 +224,15 @@ def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device,
                 fid = _all_gather_rows(torch.tensor(idx, dtype=torch.int64, device=ids.device))
                 if last:
                     fid = fid[:rem]
-                eval_ids.extend(int(x) for x in fid.cpu().tolist())
+                round_fid = [int(x) for x in fid.cpu().tolist()]
+                eval_ids.extend(round_fid)
             if last:
                 ids = ids[:rem]
-            cols[c].extend(ids.cpu().numpy())
+            mat = ids.cpu().numpy()
+            round_mats.append(mat)
+            cols[c].extend(mat)
+        if checkpoint_dir and rank == 0:
+            _save_round(checkpoint_dir, si, round_fid, round_mats)
         if on_step is not None:
             on_step(si, len(steps))
     return eval_ids, cols or []
@@ -155,7 +240,8 @@ def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device,
 
 def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *, batch_size: int,
                  pad_token_id: int, gen_kwargs: Optional[dict] = None, comm_device=None,
-                 on_step: Optional[Callable[[int, int], None]] = None, legacy_prompt_in_output: bool = False):
+                 on_step: Optional[Callable[[int, int], None]] = None, legacy_prompt_in_output: bool = False,
+                 checkpoint_dir: Optional[str] = None):
     """Transcribe items 0..n_items-1 data-parallel; returns (item_indices, predictions) in dataset order
     on every rank (``run_pseudo_labelling.py:333-344``).
 
@@ -166,7 +252,8 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
     ``tokenizer.pad_token_id`` (run_pseudo_labelling.py:339) -- for the Whisper tokenizers that is
     ``<|endoftext|>`` (the eos id, 50257), not ``generation_config.pad_token_id`` (50256), which only pads
     rows inside one generate() output.
-    ``legacy_prompt_in_output`` prepends ``legacy_prompt(...)`` to every row (needs ``language``)."""
+    ``legacy_prompt_in_output`` prepends ``legacy_prompt(...)`` to every row (needs ``language``).
+    ``checkpoint_dir``: checkpoint every gathered round there and skip rounds already written (resume)."""
     gen_kwargs = dict(gen_kwargs or {})
     prompt = None
     if legacy_prompt_in_output:
@@ -179,14 +266,15 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
         ids = model.generate(feats, **gen_kwargs)
         return [_with_prompt(ids, prompt) if prompt else ids]
 
-    eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode)
+    eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
+                                 checkpoint_dir)
     return eval_ids, (cols[0] if cols else [])
 
 
 def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *,
                            batch_size: int, text_lang_task: Sequence[tuple], pad_token_id: int,
                            gen_kwargs: Optional[dict] = None, comm_device=None,
-                           on_step: Optional[Callable[[int, int], None]] = None):
+                           on_step: Optional[Callable[[int, int], None]] = None, checkpoint_dir: Optional[str] = None):
     """``run_pseudo_labelling_v3.py:299-321``: every batch is decoded once per (text, lang, task) triple.
     Returns (item_indices, {text: predictions}) in dataset order; ``whisper_<text>`` is the column the
     reference adds (:322-323).  The encoder and cross-K/V run once per batch (``generate_multitask``) when
@@ -199,7 +287,8 @@ def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tens
             return model.generate_multitask(feats, tasks, **gen_kwargs)
         return [model.generate(feats, language=lang, task=task, **gen_kwargs) for lang, task in tasks]
 
-    eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode)
+    eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
+                                 checkpoint_dir)
     if not cols:
         cols = [[] for _ in text_lang_task]
     return eval_ids, {t[0]: c for t, c in zip(text_lang_task, cols)}

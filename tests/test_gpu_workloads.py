@@ -402,3 +402,23 @@ def test_config4_pseudo_label_engine(gold, tiny32, tmp_path):
         width = max(w, z["preds"].shape[1])
         np.testing.assert_array_equal(_pad_to(list(z["preds"]), width, pad), _pad_to(preds1, width, pad))
     print(f"\nconfig4 pseudo_label: W=1 and W=2 (gloo, 2 processes on cuda:0) agree on {N_ITEMS} items")
+
+
+def test_config4_pseudo_label_resume_engine(tiny32, tmp_path):
+    """Resume by round over the HIP engine: a run checkpoints its gathered rounds; after the last round's file
+    is lost the rerun decodes that round only and returns the uninterrupted run's predictions."""
+    from kwhisper.pseudo_label import pseudo_label
+
+    pad = tiny32.generation_config.eos_token_id
+    ck = str(tmp_path / "ck")
+    ids1, preds1 = pseudo_label(tiny32, _item_features, N_ITEMS, batch_size=BS, gen_kwargs=GEN_KW, pad_token_id=pad,
+                                checkpoint_dir=ck)
+    last = sorted(f for f in os.listdir(ck) if f.startswith("round_"))[-1]
+    os.remove(os.path.join(ck, last))
+    seen = []
+    ids2, preds2 = pseudo_label(tiny32, lambda idx: (seen.append(list(idx)), _item_features(idx))[1], N_ITEMS,
+                                batch_size=BS, gen_kwargs=GEN_KW, pad_token_id=pad, checkpoint_dir=ck)
+    assert seen == [[8, 9, 0, 1]]  # only the lost (wrapped) round was decoded again
+    assert ids2 == ids1 == list(range(N_ITEMS))
+    for a, b in zip(preds1, preds2):
+        np.testing.assert_array_equal(a, b)

@@ -223,3 +223,78 @@ def test_transcription_arrow_column_matches_datasets(tmp_path):
     with pa.OSFile(p, "rb") as f:
         back = pa.ipc.open_stream(f).read_all()
     assert back.equals(t)
+
+
+# ---- resume by round (SURVEY.md §5 checkpoint / resume) ---------------------------------------------------
+class _CountingModel(_StubModel):
+    def __init__(self):
+        self.batches = []
+
+    def generate(self, feats, **kw):
+        self.batches.append(feats[:, 0].long().tolist())
+        return super().generate(feats, **kw)
+
+
+def _same(a, b):
+    assert a[0] == b[0]
+    assert len(a[1]) == len(b[1])
+    for x, y in zip(a[1], b[1]):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_resume_skips_checkpointed_rounds(tmp_path):
+    ck = str(tmp_path / "ck")
+    n, bs = 23, 4  # 6 rounds, the last one ragged
+    ref = pseudo_label(_StubModel(), _features, n, batch_size=bs, pad_token_id=PAD)
+    m1 = _CountingModel()
+    run1 = pseudo_label(m1, _features, n, batch_size=bs, pad_token_id=PAD, checkpoint_dir=ck)
+    _same(run1, ref)
+    assert len(m1.batches) == 6
+    assert sorted(os.listdir(ck)) == ["plan.json"] + [f"round_{i:06d}.npz" for i in range(6)]
+    # a crash after round 3: rounds 4 and 5 never reached the disk
+    for i in (4, 5):
+        os.remove(os.path.join(ck, f"round_{i:06d}.npz"))
+    m2 = _CountingModel()
+    run2 = pseudo_label(m2, _features, n, batch_size=bs, pad_token_id=PAD, checkpoint_dir=ck)
+    _same(run2, ref)
+    assert m2.batches == [list(range(16, 20)), [20, 21, 22, 0]]  # only the missing rounds (the last wraps)
+    m3 = _CountingModel()  # everything on disk: nothing is decoded
+    _same(pseudo_label(m3, _features, n, batch_size=bs, pad_token_id=PAD, checkpoint_dir=ck), ref)
+    assert m3.batches == []
+
+
+def test_resume_refuses_another_plan(tmp_path):
+    ck = str(tmp_path / "ck")
+    pseudo_label(_StubModel(), _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=ck)
+    with pytest.raises(ValueError, match="another plan"):
+        pseudo_label(_StubModel(), _features, 10, batch_size=3, pad_token_id=PAD, checkpoint_dir=ck)
+
+
+def _resume_worker(rank, world, port, n, bs, ck, out_dir, tag):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        m = _CountingModel()
+        ids, preds = pseudo_label(m, _features, n, batch_size=bs, pad_token_id=PAD, checkpoint_dir=ck)
+        np.savez(os.path.join(out_dir, f"{tag}{rank}.npz"), ids=np.array(ids),
+                 preds=np.array([p.tolist() + [-1] * (16 - len(p)) for p in preds]),
+                 decoded=np.array([i for b in m.batches for i in b] or [-1]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_resume_gloo_world2(tmp_path):
+    import torch.multiprocessing as mp
+
+    n, bs = 13, 2  # rounds of 2 x 2 items: 4 rounds, the last one wrapped
+    ck = str(tmp_path / "ck")
+    mp.spawn(_resume_worker, args=(2, _free_port(), n, bs, ck, str(tmp_path), "a"), nprocs=2, join=True)
+    os.remove(os.path.join(ck, "round_000002.npz"))
+    mp.spawn(_resume_worker, args=(2, _free_port(), n, bs, ck, str(tmp_path), "b"), nprocs=2, join=True)
+    for r in range(2):
+        a, b = np.load(tmp_path / f"a{r}.npz"), np.load(tmp_path / f"b{r}.npz")
+        assert a["ids"].tolist() == b["ids"].tolist() == list(range(n))
+        np.testing.assert_array_equal(a["preds"], b["preds"])
+        # the second run decoded round 2 only: items 8-9 on rank 0, 10-11 on rank 1
+        assert b["decoded"].tolist() == [[8, 9], [10, 11]][r]

@@ -30,7 +30,7 @@ static void fill(unsigned short* d, size_t n, unsigned seed) {
 
 int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 48000, N = argc > 2 ? atoi(argv[2]) : 1280, K = argc > 3 ? atoi(argv[3]) : 1280;
-  const int mode = argc > 4 ? atoi(argv[4]) : 0;  // 0 store bf16, 1 bias+GELU bf16, 2 residual add into f32
+  const int mode = argc > 4 ? atoi(argv[4]) : 0;  // 0 store bf16, 1 bias+GELU bf16, 2 residual add into f32, 3 bias + store bf16
   unsigned short *A, *W, *C;
   float* bias;
   hipMalloc(&A, (size_t)M * K * 2);
@@ -50,6 +50,7 @@ int main(int argc, char** argv) {
   a.dtype = KW_DT_BF16; a.c_dtype = KW_DT_BF16; a.A = A; a.lda = K; a.W = W; a.C = C; a.ldc = N;
   a.M = M; a.N = N; a.K = K; a.epilogue = KW_EPI_STORE; a.scale = 1.f;
   if (mode == 1) { a.gelu = 1; a.bias = bias; }
+  if (mode == 3) a.bias = bias;  // bias, no GELU
   if (mode == 2) { a.epilogue = KW_EPI_RESID; a.c_dtype = KW_DT_F32; a.bias = bias; }
   for (int i = 0; i < 20; ++i) kw_gemm(&a, 0);
   hipEvent_t e0, e1;
