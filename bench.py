@@ -242,10 +242,11 @@ def main():
             for li in range(n_dec):
                 ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[2 * li], sess.cross[2 * li + 1], S, attn_out, ws)
 
-        cross_kernel = "cross_attn_kernel"
+        cross_kernel = "cross_attn_dma_kernel"
         cross_t = time_fn(cross_all_layers, max(1, iters // 4)) / n_dec
         cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
-        cross_note = "cross_attn_kernel (decoder cross-attention K/V stream, one launch per layer; rocprof name)"
+        cross_note = ("cross_attn_dma_kernel (decoder cross-attention K/V stream, K by LDS-DMA, one launch per layer; "
+                      "rocprof name)")
     feats = fe.extract(audio)
     enc_t = time_fn(lambda: eng.encode(feats), 3)
     step_graph = sess._graph

@@ -598,6 +598,129 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q
   publish_and_combine<T>(ws + (int64_t)row * ns * (HD + 2), cnt + row, ns, split, m, l, o, orow, &last);
 }
 
+// Cross-attention, bf16, one query row per (row, chunk) workgroup -- as cross_attn_kernel, but the chunk's K
+// (XA_DMA >= 1) and V (XA_DMA == 2) rows arrive by LDS-DMA (global_load_lds_dwordx4, non-temporal) instead of
+// register loads (MI355X_MICROARCH "ldsdma-fill": the LDS-DMA stream runs closer to the HBM rate).  Large-v3
+// B = 32 (tools/lab/xa_dma_check.py, one box, two rounds): K by LDS-DMA 44.4-44.6 us vs 45.4-45.6 for register
+// loads; K and V by LDS-DMA 50.3 us (64 KB of LDS per workgroup: 2 per CU instead of 5).  Wave w's DMA instruction j moves keys k0 + 32 j + 8 w + (0..7) (1 KB,
+// lane = (key, 16-B piece)) to LDS piece 4 j + w and each lane reads back exactly its own 16 B, so the score /
+// softmax / value arithmetic is attend_chunk's, operation for operation (results bitwise equal).
+#ifndef KW_XA_DMA
+#define KW_XA_DMA 1  // 0: register loads only (cross_attn_kernel); 2: V by LDS-DMA too (64 KB LDS: slower, 2 WGs/CU)
+#endif
+constexpr int XA_DMA = KW_XA_DMA;
+
+__device__ __forceinline__ void glds16_nt(const void* g, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)lds_base, 16, 0, 2);
+}
+__device__ __forceinline__ u32x4 lds_rd16(const char* p) {
+  u32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(lds_u32(p)) : "memory");
+  return v;
+}
+
+__global__ __launch_bounds__(256) void cross_attn_dma_kernel(const bf16_t* __restrict__ q, int q_len, int H,
+                                                             const bf16_t* __restrict__ kc,
+                                                             const bf16_t* __restrict__ vc, int S, int chunk,
+                                                             float* __restrict__ ws, int* __restrict__ cnt,
+                                                             bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char kv[(XA_DMA == 2 ? 2 : 1) * 32 * 1024];
+  __shared__ float red[4][64];
+  __shared__ float stat[8];
+  __shared__ int last;
+  const int row = blockIdx.x, split = blockIdx.y, ns = gridDim.y;
+  const int h = row % H, bq = row / H, b = bq / q_len;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
+  const int k0 = split * chunk, k1 = min(S, k0 + chunk);
+  const bf16_t* kb = kc + ((int64_t)b * H + h) * S * HD;
+  const bf16_t* vb = vc + ((int64_t)b * H + h) * S * HD;
+  // the query first (inline asm: hipcc would otherwise drain every LDS-DMA in flight before its use)
+  u32x4 qraw;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(qraw) : "v"(q + (int64_t)bq * H * HD + h * HD + sub * 8) : "memory");
+  // every group j is issued (clamped keys: the host guarantees k1 - k0 > 224, so group 7 has valid keys)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) glds16_nt(kb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8, kv + (4 * j + wave) * 1024);
+  Row8<bf16_t> vr[8];
+  if constexpr (XA_DMA == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      glds16_nt(vb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8, kv + 32 * 1024 + (4 * j + wave) * 1024);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vr[j] = ld_row8<bf16_t>(vb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8);
+  }
+  asm volatile("s_waitcnt vmcnt(8)" : "+v"(qraw) :: "memory");  // q and this wave's K pieces landed (V may fly)
+  float qv[8];
+  {
+    Row8<bf16_t> qr;
+    qr.u[0] = qraw;
+    unpack8<bf16_t>(qr, qv);
+  }
+  __builtin_amdgcn_s_barrier();
+  Row8<bf16_t> kr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) kr[j].u[0] = lds_rd16(kv + (4 * j + wave) * 1024 + lane * 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kr[0].u[0]), "+v"(kr[1].u[0]), "+v"(kr[2].u[0]), "+v"(kr[3].u[0]),
+               "+v"(kr[4].u[0]), "+v"(kr[5].u[0]), "+v"(kr[6].u[0]), "+v"(kr[7].u[0]));
+  float sc[8];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    float kf[8];
+    unpack8<bf16_t>(kr[j], kf);
+    float sj = 0.f;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kf[i], sj);
+    sj = kw_sum8(sj);
+    sc[j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
+    mx = fmaxf(mx, sc[j]);
+  }
+  mx = wave_max(mx);
+  if (lane == 0) stat[wave] = mx;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const float m = fmaxf(fmaxf(stat[0], stat[1]), fmaxf(stat[2], stat[3]));
+  if constexpr (XA_DMA == 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V pieces (only it reads them)
+    __builtin_amdgcn_s_barrier();
+  }
+  if constexpr (XA_DMA == 2) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vr[j].u[0] = lds_rd16(kv + 32 * 1024 + (4 * j + wave) * 1024 + lane * 16);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0].u[0]), "+v"(vr[1].u[0]), "+v"(vr[2].u[0]), "+v"(vr[3].u[0]),
+                 "+v"(vr[4].u[0]), "+v"(vr[5].u[0]), "+v"(vr[6].u[0]), "+v"(vr[7].u[0]));
+  }
+  float lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[j] - m) : 0.f;
+    lsum += pj;
+    float vv[8];
+    unpack8<bf16_t>(vr[j], vv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = kw_sum_hi(acc[i]);
+  lsum = wave_sum(lsum) * 0.125f;
+  if (lane < 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
+  }
+  if (lane == 0) stat[4 + wave] = lsum;
+  __syncthreads();
+  const float l = (stat[4] + stat[5]) + (stat[6] + stat[7]);
+  const float o = tid < HD ? (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]) : 0.f;
+  bf16_t* orow = out + (int64_t)bq * H * HD + h * HD;
+  if (ns == 1) {
+    if (tid < HD) TypeIO<bf16_t>::st(orow + tid, o / l);
+    return;
+  }
+  publish_and_combine<bf16_t>(ws + (int64_t)row * ns * (HD + 2), cnt + row, ns, split, m, l, o, orow, &last);
+}
+
 // Cross-attention for several query rows of one item (the prefill's P prompt positions, and the beams of
 // an item, which all read the same encoder K/V): QN rows per workgroup share ONE pass over the chunk's
 // K/V (the one-row kernel above reads it once per row).  Per row the arithmetic is attend_chunk's,
@@ -1127,7 +1250,10 @@ extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q
     const dim3 gm((unsigned)(B * ((q_len + 7) / 8) * H), (unsigned)ns);
     hipLaunchKernelGGL((cross_attn_multi_kernel<bf16_t, 8>), gm, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
-  } else if (dtype == KW_DT_BF16)
+  } else if (dtype == KW_DT_BF16 && XA_DMA && chunk > 224 && chunk <= 256 && S - (int64_t)(ns - 1) * chunk > 224)
+    hipLaunchKernelGGL(cross_attn_dma_kernel, grid, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
+                       (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
+  else if (dtype == KW_DT_BF16)
     hipLaunchKernelGGL(cross_attn_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
   else
