@@ -1,6 +1,6 @@
 #!/usr/bin/env python
-"""Lab (not product): kw_cross_attn_step of two builds of libkwhisper.so (ctypes, one process) on the same
-inputs -- bitwise comparison -- and their timing over 32 layers' K/V.   python tools/lab/xa_dma_check.py A.so B.so"""
+"""Lab (not product): kw_cross_attn_step of several builds of libkwhisper.so (ctypes, one process) on the same
+inputs -- bitwise comparison -- and their timing over 32 layers' K/V.   python tools/lab/xa_dma_check.py A.so B.so [...]"""
 import ctypes
 import json
 import sys
@@ -19,7 +19,8 @@ def load(path):
 
 
 def main():
-    libs = [load(p) for p in sys.argv[1:3]]
+    paths = sys.argv[1:]
+    libs = [load(p) for p in paths]
     B, H, S, hd, nl = 32, 20, 1500, 64, 16
     g = torch.Generator(device="cuda").manual_seed(0)
     cross = [torch.randn(2, B, H, S, hd, device="cuda", generator=g).bfloat16() for _ in range(nl)]
@@ -50,9 +51,10 @@ def main():
                 run(c)
         e1.record(s)
         e1.synchronize()
-        res[sys.argv[1 + li]] = round(e0.elapsed_time(e1) * 1e3 / (10 * nl), 2)
-    res["bitwise_equal"] = bool(torch.equal(outs[0], outs[1]))
-    res["max_abs_diff"] = float((outs[0].float() - outs[1].float()).abs().max())
+        res[paths[li]] = round(e0.elapsed_time(e1) * 1e3 / (10 * nl), 2)
+    for li in range(1, len(libs)):
+        res[f"{paths[li]} vs {paths[0]}"] = {"bitwise_equal": bool(torch.equal(outs[0], outs[li])),
+                                             "max_abs_diff": float((outs[0].float() - outs[li].float()).abs().max())}
     print(json.dumps(res))
 
 
