@@ -49,14 +49,34 @@ __device__ __forceinline__ void bins3(uint64_t k, uint64_t& c0, uint64_t& c1, ui
   c1 = h1;
   c2 = l1 > c2 ? l1 : c2;
 }
+// wave maximum of 64-bit keys on the VALU: DPP within 16-lane rows (quad_perm ^1 / ^2, then half-row and
+// row mirrors once the quads / halves are uniform), v_permlane16/32_swap across rows -- no ds_bpermute round
+// trips (a maximum is exact, so any reduction tree gives the butterfly's result)
+template <int CTRL>
+__device__ __forceinline__ uint64_t u64_max_dpp(uint64_t k) {
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(k >> 32), CTRL, 0xF, 0xF, false);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)k, CTRL, 0xF, 0xF, false);
+  const uint64_t o = ((uint64_t)hi << 32) | lo;
+  return o > k ? o : k;
+}
+__device__ __forceinline__ uint64_t u64_max_swap16(uint64_t k) {
+  const auto h = __builtin_amdgcn_permlane16_swap((uint32_t)(k >> 32), (uint32_t)(k >> 32), false, false);
+  const auto l = __builtin_amdgcn_permlane16_swap((uint32_t)k, (uint32_t)k, false, false);
+  const uint64_t a = ((uint64_t)h[0] << 32) | l[0], b = ((uint64_t)h[1] << 32) | l[1];
+  return a > b ? a : b;
+}
+__device__ __forceinline__ uint64_t u64_max_swap32(uint64_t k) {
+  const auto h = __builtin_amdgcn_permlane32_swap((uint32_t)(k >> 32), (uint32_t)(k >> 32), false, false);
+  const auto l = __builtin_amdgcn_permlane32_swap((uint32_t)k, (uint32_t)k, false, false);
+  const uint64_t a = ((uint64_t)h[0] << 32) | l[0], b = ((uint64_t)h[1] << 32) | l[1];
+  return a > b ? a : b;
+}
 __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint32_t hi = (uint32_t)__shfl_xor((int)(k >> 32), o, 64), lo = (uint32_t)__shfl_xor((int)(uint32_t)k, o, 64);
-    const uint64_t ok = ((uint64_t)hi << 32) | lo;
-    k = ok > k ? ok : k;
-  }
-  return k;
+  k = u64_max_dpp<0xB1>(k);   // quad_perm [1,0,3,2]
+  k = u64_max_dpp<0x4E>(k);   // quad_perm [2,3,0,1]
+  k = u64_max_dpp<0x141>(k);  // row_half_mirror
+  k = u64_max_dpp<0x140>(k);  // row_mirror
+  return u64_max_swap32(u64_max_swap16(k));
 }
 
 __global__ __launch_bounds__(ST) void beam_logprobs_kernel(kw_beam_logprobs_args a) {
@@ -211,7 +231,6 @@ __device__ __forceinline__ float bl_sum(float v, float* sh) {
 }
 
 __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logprobs_args a) {
-  __shared__ int shi[2 * (BT_S / 64)];
   __shared__ RowState st_sh;
   __shared__ float pub[BPART];
   if (*a.done) return;
@@ -230,26 +249,32 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
     const int v = v0 + tid + u * BT_S;
     xv[u] = v < v1 ? x[v] : -INFINITY;
   }
-  // row state from the history (as kwp::row_state, BT_S threads)
-  int lsp = -1;
-  for (int p = a.begin_index + tid; p < L; p += BT_S)
-    if (ids[p] >= a.ts_begin) lsp = max(lsp, p);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) lsp = max(lsp, __shfl_xor(lsp, o, 64));
-  if ((tid & 63) == 0) shi[tid >> 6] = lsp;
+  // row state from the history (as kwp::row_state, BT_S threads): the last timestamp position travels with
+  // its token in one 64-bit key (no dependent reload), the last two tokens are read up front
+  const int n_hist = L - a.begin_index;
+  const int64_t tok_l1 = n_hist >= 1 ? ids[L - 1] : 0, tok_l2 = n_hist >= 2 ? ids[L - 2] : 0;
+  uint64_t lkey = 0;  // ((position + 1) << 32) | token of the row's last timestamp
+  for (int p = a.begin_index + tid; p < L; p += BT_S) {
+    const int64_t t = ids[p];
+    if (t >= a.ts_begin) lkey = ((uint64_t)(uint32_t)(p + 1) << 32) | (uint32_t)t;
+  }
+  lkey = wave_max_u64(lkey);
+  __shared__ uint64_t lkeys[BT_S / 64];
+  if ((tid & 63) == 0) lkeys[tid >> 6] = lkey;
   __syncthreads();
   if (tid == 0) {
-    int lp = shi[0];
-    for (int i = 1; i < BT_S / 64; ++i) lp = max(lp, shi[i]);
+    uint64_t lk = lkeys[0];
+    for (int i = 1; i < BT_S / 64; ++i) lk = lkeys[i] > lk ? lkeys[i] : lk;
+    const int lp = (int)(lk >> 32) - 1;
+    const int lp_tok = (int)(uint32_t)lk;
     RowState st;
     st.L = L; st.begin = a.begin_index; st.ts_begin = a.ts_begin; st.no_ts = a.no_ts_id; st.eos = a.eos_id;
     st.rt = a.return_timestamps; st.max_init = a.max_initial_ts; st.ban_text = 0;
-    const int n = L - a.begin_index;
     st.first_step = (L == a.begin_index);
-    st.last_ts = n >= 1 && ids[L - 1] >= a.ts_begin;
-    st.pen_ts = n < 2 || ids[L - 2] >= a.ts_begin;
+    st.last_ts = n_hist >= 1 && tok_l1 >= a.ts_begin;
+    st.pen_ts = n_hist < 2 || tok_l2 >= a.ts_begin;
     st.has_stamp = lp >= 0;
-    st.stamp_lo = st.has_stamp ? ((st.last_ts && !st.pen_ts) ? (int)ids[lp] : (int)ids[lp] + 1) : 0;
+    st.stamp_lo = st.has_stamp ? ((st.last_ts && !st.pen_ts) ? lp_tok : lp_tok + 1) : 0;
     st_sh = st;
   }
   __syncthreads();
@@ -325,7 +350,11 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
   // the slice's KP best processed scores (all tokens; and timestamps only, for the text-ban case):
   // each wave takes its own kp best by shuffle-only rounds (no workgroup barrier per round), then wave 0
   // takes the slice's kp best of the waves' 8 x kp
+#ifdef KW_BEAM_LAB_KP
+  const int kp = KW_BEAM_LAB_KP;  // lab: round count sweep (results wrong below K + 4)
+#else
   const int kp = min(K + 4, KP);
+#endif
   const int lane = tid & 63, wv = tid >> 6;
   __shared__ uint64_t wck[2][BT_S / 64][KP];
 #ifdef KW_BEAM_LAB_SKIP_TOPK
@@ -469,28 +498,29 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
       }
     }
   }
-  for (int j = 0; j < K; ++j) {
-    float bv = c[0];
-    int bi = ci3[0], bs = 0;
-    if (better(c[1], ci3[1], bv, bi)) { bv = c[1]; bi = ci3[1]; bs = 1; }
-    if (better(c[2], ci3[2], bv, bi)) { bv = c[2]; bi = ci3[2]; bs = 2; }
-    float gv = bv;
-    int gi = bi, gl = lane;
+  // k rounds of a wave maximum over 64-bit (log-prob, token) keys ordered like better() (token indices are
+  // unique, so exactly one lane holds the winner; it writes its own f32 value and retires the key)
+  uint64_t kk[3];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const float ov = __shfl_xor(gv, o, 64);
-      const int oi = __shfl_xor(gi, o, 64), ol = __shfl_xor(gl, o, 64);
-      if (better(ov, oi, gv, gi)) { gv = ov; gi = oi; gl = ol; }
+  for (int t = 0; t < 3; ++t) kk[t] = ci3[t] != 0x7fffffff ? bkey(c[t], ci3[t]) : 0;
+  for (int j = 0; j < K; ++j) {
+    uint64_t b = kk[0] > kk[1] ? kk[0] : kk[1];
+    b = b > kk[2] ? b : kk[2];
+    const uint64_t g = wave_max_u64(b);
+    if (g == 0) {  // no candidate left (cannot happen with a sane config): as the reference's -inf / 0
+      if (lane == 0) {
+        a.cand_val[(int64_t)r * K + j] = -INFINITY;
+        a.cand_idx[(int64_t)r * K + j] = 0;
+      }
+      continue;
     }
-    if (lane == gl && gi == bi && bi != 0x7fffffff) {
-      if (bs == 0) { c[0] = -INFINITY; ci3[0] = 0x7fffffff; }
-      else if (bs == 1) { c[1] = -INFINITY; ci3[1] = 0x7fffffff; }
-      else { c[2] = -INFINITY; ci3[2] = 0x7fffffff; }
-    }
-    if (lane == 0) {
-      a.cand_val[(int64_t)r * K + j] = gv;
-      a.cand_idx[(int64_t)r * K + j] = gi == 0x7fffffff ? 0 : gi;
-    }
+#pragma unroll
+    for (int t = 0; t < 3; ++t)
+      if (kk[t] == g) {
+        a.cand_val[(int64_t)r * K + j] = c[t];
+        a.cand_idx[(int64_t)r * K + j] = ci3[t];
+        kk[t] = 0;
+      }
   }
 }
 
