@@ -610,6 +610,15 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q
 #endif
 constexpr int XA_DMA = KW_XA_DMA;
 
+// a workgroup barrier without __syncthreads()'s fence (which waits vmcnt(0), draining loads still in flight);
+// compiler barriers on both sides keep every memory access (LDS reads of DMA'd data) on its side
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("" ::: "memory");
+}
 __device__ __forceinline__ void glds16_nt(const void* g, char* lds_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
                                    (__attribute__((address_space(3))) void*)lds_base, 16, 0, 2);
@@ -658,7 +667,7 @@ __global__ __launch_bounds__(256) void cross_attn_dma_kernel(const bf16_t* __res
     qr.u[0] = qraw;
     unpack8<bf16_t>(qr, qv);
   }
-  __builtin_amdgcn_s_barrier();
+  raw_barrier();
   Row8<bf16_t> kr[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) kr[j].u[0] = lds_rd16(kv + (4 * j + wave) * 1024 + lane * 16);
@@ -680,11 +689,11 @@ __global__ __launch_bounds__(256) void cross_attn_dma_kernel(const bf16_t* __res
   mx = wave_max(mx);
   if (lane == 0) stat[wave] = mx;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
+  raw_barrier();
   const float m = fmaxf(fmaxf(stat[0], stat[1]), fmaxf(stat[2], stat[3]));
   if constexpr (XA_DMA == 2) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V pieces (only it reads them)
-    __builtin_amdgcn_s_barrier();
+    raw_barrier();
   }
   if constexpr (XA_DMA == 2) {
 #pragma unroll

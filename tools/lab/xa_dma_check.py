@@ -21,20 +21,22 @@ def load(path):
 def main():
     paths = sys.argv[1:]
     libs = [load(p) for p in paths]
-    B, H, S, hd, nl = 32, 20, 1500, 64, 16
+    import os
+    B, H, S, hd, nl = int(os.environ.get("XA_B", 32)), 20, 1500, 64, 16
+    QL = int(os.environ.get("XA_QLEN", 1))  # rows per item (beams: the MFMA kernel from 5)
     g = torch.Generator(device="cuda").manual_seed(0)
     cross = [torch.randn(2, B, H, S, hd, device="cuda", generator=g).bfloat16() for _ in range(nl)]
-    q = (torch.randn(B, H * hd, device="cuda", generator=g) * 2).bfloat16()
-    wsb = libs[0].kw_cross_attn_workspace(B, 1, H, hd, S)
+    q = (torch.randn(B * QL, H * hd, device="cuda", generator=g) * 2).bfloat16()
+    wsb = libs[0].kw_cross_attn_workspace(B, QL, H, hd, S)
     res = {}
     outs = []
     s = torch.cuda.current_stream()
     for li, lib in enumerate(libs):
         ws = torch.zeros(wsb // 4 + 1, device="cuda")
-        out = torch.empty(B, H * hd, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty(B * QL, H * hd, device="cuda", dtype=torch.bfloat16)
 
         def run(c):
-            rc = lib.kw_cross_attn_step(1, q.data_ptr(), B, 1, H, hd, c[0].data_ptr(), c[1].data_ptr(), S,
+            rc = lib.kw_cross_attn_step(1, q.data_ptr(), B, QL, H, hd, c[0].data_ptr(), c[1].data_ptr(), S,
                                         out.data_ptr(), ws.data_ptr(), wsb, s.cuda_stream)
             assert rc == 0
         run(cross[0])
