@@ -127,22 +127,6 @@ typedef struct {
 
 int kw_dec_linear(const kw_dec_linear_args* args, kw_stream_t stream);
 size_t kw_dec_linear_workspace_bytes(int64_t N, int64_t K);
-
-/* Consecutive dependent decode linears of one decoder layer in ONE launch: self_attn.out_proj ->
- * encoder_attn.q_proj (after encoder_attn_layer_norm) and encoder_attn.out_proj -> fc1 -> fc2 (after
- * final_layer_norm), TF modeling_whisper.py:476-503.  phases[i] is a kw_dec_linear block whose activations
- * are phase i-1's output; every phase has the same M <= 32 rows, N % 32 == 0 and no x groups.  Results are
- * bitwise those of kw_dec_linear on each block in turn (same geometry and arithmetic); the launch only lets
- * each phase's weight stream start before the phase it depends on has finished.
- * sync: >= kw_dec_chain_sync_bytes() bytes, zero-filled before first use; calls leave the counters zeroed.
- * One sync area serves every chain launched on one stream.  A chain kw_dec_chain_supported() rejects
- * returns KW_EUNSUPPORTED (launch the phases with kw_dec_linear instead).  kw_dec_chain_status() syncs the
- * stream, sets *flagged to the sync area's error word and clears it: nonzero = a phase waited past its bound
- * (its results are wrong). */
-int kw_dec_chain(const kw_dec_linear_args* phases, int n_phases, void* sync, size_t sync_bytes, kw_stream_t stream);
-int kw_dec_chain_supported(const kw_dec_linear_args* phases, int n_phases);
-size_t kw_dec_chain_sync_bytes(void);
-int kw_dec_chain_status(void* sync, int* flagged, kw_stream_t stream);
 /* W [N][K] bf16 -> packed [ceil(N/32)*2][K/32][64 lanes][8] bf16 (columns >= N zero); K % 32 == 0. */
 int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed, kw_stream_t stream);
 size_t kw_packed_weight_bytes(int64_t N, int64_t K);

@@ -24,7 +24,6 @@
 // Everything is bitwise deterministic: no float atomics, every reduction in a fixed order.
 #include <stdio.h>
 #include <stdlib.h>
-#include <string.h>
 
 #include <algorithm>
 #include <array>
@@ -513,410 +512,6 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
   }
 }
 
-// ---- chained decode linears: consecutive dependent linears of one layer in ONE launch ------------------
-// (o -> cross q) and (cross out -> fc1 -> fc2) at M <= 32 rows.  Each linear is a phase: a contiguous
-// range of blockIdx.x with dec_linear_kernel's geometry and arithmetic operation for operation (same
-// fragments, MFMA order, wave-ordered reduction, K-split seam, epilogue), so results are bitwise those of
-// the separate launches.  What changes is WHEN the work can start: a phase's workgroups issue their weight
-// loads (the HBM stream, independent of the previous phase) as soon as they are resident, and only then
-// wait for the phase before them; the kernel boundary they replace serialised the weight round trip behind
-// the previous linear's tail.  Hand-off (MI355X_MICROARCH "Valid forms", first table row): a producer
-// workgroup's storing wave 0 writes every handed-off byte with sc1 (write-through) 4-B stores, waits
-// vmcnt(0), then lane 0 adds 1 to its shard (blockIdx % 8, one 128-B line each) of the phase counter;
-// a consumer's wave 0 polls the 8 shards with sc1 loads until they sum to the producer's workgroup count,
-// a workgroup barrier releases the other waves, and every load of handed-off bytes (activations, the
-// residual h) is an sc1 load.  Forward progress: a workgroup only waits on workgroups with lower
-// blockIdx.x (earlier phases), which are dispatched before it; the wait is bounded (CH_SPIN_MAX polls, then
-// the error word is set and the kernel runs on) so a broken assumption shows as a flagged wrong result,
-// never a hang.  The chain's last workgroup (two-level count over the final phase) zeroes every counter.
-constexpr int CH_MAXPH = 3, CH_SHARDS = 8, CH_LINE = 32;  // ints per counter line (128 B)
-#ifndef KW_CH_XLD
-#define KW_CH_XLD 16  // lab: cache policy of the activation loads (16 = sc1)
-#endif
-#ifndef KW_CH_PLAIN_ST
-#define KW_CH_PLAIN_ST 0  // lab: plain epilogue stores (NOT coherent across XCDs: timing only)
-#endif
-#ifndef KW_CH_SLEEP
-#define KW_CH_SLEEP 2
-#endif
-constexpr int CH_SPIN_MAX = 1 << 20;
-
-struct ChainPh {
-  DecP p;
-  int ksn, ncg, nwg, off, nw;
-};
-struct ChainP {
-  ChainPh ph[CH_MAXPH];
-  int nph;
-  int* sync;  // [CH_MAXPH][CH_SHARDS] counters, then the top counter and the error word, CH_LINE ints apart
-#ifdef KW_CH_STAMPS
-  unsigned long long* stamps;  // lab: [blockIdx][8] s_memrealtime stamps of wave 0
-#endif
-};
-#ifdef KW_CH_STAMPS
-#define CH_STAMP(i) \
-  if (threadIdx.x == 0 && cp.stamps) cp.stamps[(int64_t)blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();
-#else
-#define CH_STAMP(i)
-#endif
-__device__ __forceinline__ int* ch_cnt(int* sync, int ph, int shard) { return sync + (ph * CH_SHARDS + shard) * CH_LINE; }
-__device__ __forceinline__ int* ch_top(int* sync) { return sync + CH_MAXPH * CH_SHARDS * CH_LINE; }
-__device__ __forceinline__ int* ch_err(int* sync) { return sync + (CH_MAXPH * CH_SHARDS + 1) * CH_LINE; }
-
-template <typename T>
-__device__ __forceinline__ T ld_sc1(const T* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* p, T v) {
-#if KW_CH_PLAIN_ST
-  *p = v;
-#else
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-}
-
-// wave 0: poll phase ph's 8 counter shards (lanes 0..7, sc1 loads) until they sum to target
-__device__ __forceinline__ void ch_wait(int* sync, int ph, int target, int lane) {
-  for (int it = 0;; ++it) {
-    int v = lane < CH_SHARDS ? ld_sc1(ch_cnt(sync, ph, lane)) : 0;
-    v += __shfl_xor(v, 1, 64);
-    v += __shfl_xor(v, 2, 64);
-    v += __shfl_xor(v, 4, 64);
-    if (__shfl(v, 0, 64) >= target) return;
-    if (it >= CH_SPIN_MAX) {
-      if (lane == 0) __hip_atomic_store(ch_err(sync), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(KW_CH_SLEEP);
-  }
-}
-
-// wave 0 lane 0, after the workgroup's stores have drained: count this workgroup done; the chain's last
-// workgroup (last phase, last of its shard, last shard) zeroes every counter for the next launch
-__device__ __forceinline__ void ch_signal(const ChainP& cp, int phi, int bl) {
-  const int s = bl % CH_SHARDS;
-  const int prev = __hip_atomic_fetch_add(ch_cnt(cp.sync, phi, s), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (phi != cp.nph - 1) return;
-  const int nwg = cp.ph[phi].nwg;
-  if (prev != (nwg - s + CH_SHARDS - 1) / CH_SHARDS - 1) return;
-  if (__hip_atomic_fetch_add(ch_top(cp.sync), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != min(nwg, CH_SHARDS) - 1)
-    return;
-  for (int q = 0; q < cp.nph; ++q)
-    for (int s2 = 0; s2 < CH_SHARDS; ++s2)
-      __hip_atomic_store(ch_cnt(cp.sync, q, s2), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(ch_top(cp.sync), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ void ch_raw_barrier() {  // s_barrier without the vmcnt(0) drain of __syncthreads
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-
-template <int KTM_, int NCB_, bool LNA_, int EPI_, typename TC_>
-struct ChCfg {
-  static constexpr int KTM = KTM_, NCB = NCB_, EPI = EPI_;
-  static constexpr bool LNA = LNA_;
-  typedef TC_ TC;
-};
-
-template <class CF>
-__device__ __forceinline__ void ch_phase(const ChainP& cp, int phi, int bl, f32x4 (&red)[MAXW][2][2][64],
-                                         float (&rpart)[MAXW][32][2], float (&rstat)[32][2]) {
-  constexpr int KTM = CF::KTM, NCB = CF::NCB, EPI = CF::EPI;
-  constexpr bool LNA = CF::LNA;
-  typedef typename CF::TC TC;
-  const ChainPh& ph = cp.ph[phi];
-  const DecP& p = ph.p;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = ph.nw;
-  const bool act = wave < nw;  // waves past the phase's count only join the barriers
-  const int ksn = ph.ksn, cg = bl % ph.ncg, ks = bl / ph.ncg;
-  const int nkt = p.K >> 5;
-  const int nsl = ksn * nw, sl = ks * nw + min(wave, nw - 1);
-  const int kt0 = (nkt * sl) / nsl, kt1 = (nkt * (sl + 1)) / nsl;
-  const int ktl = max(kt1 - 1, kt0);
-  const int M = p.M;
-  const int arow = lane & 15;
-  CH_STAMP(0);
-
-  // 1. this wave's weights in flight (the HBM stream: no dependence on the previous phase)
-  bf16x8 w[NCB][KTM], a0[KTM], a1[KTM];
-  if (act) {
-#pragma unroll
-    for (int c = 0; c < NCB; ++c)
-#pragma unroll
-      for (int u = 0; u < KTM; ++u)
-        w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)(cg * NCB + c) * nkt + min(kt0 + u, ktl)) * 64 + lane);
-  }
-  float hold[NCB][2][4], ebias[NCB], ecsum[NCB];
-#pragma unroll
-  for (int c = 0; c < NCB; ++c) {
-    const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
-    ebias[c] = p.bias ? p.bias[n] : 0.f;
-    ecsum[c] = LNA ? p.ln_colsum[n] : 0.f;
-  }
-
-  // 2. wait for the phase before (its workgroups all have lower blockIdx.x)
-  if (phi > 0) {
-    if (wave == 0) ch_wait(cp.sync, phi - 1, cp.ph[phi - 1].nwg, lane);
-    ch_raw_barrier();
-  }
-  CH_STAMP(1);
-
-  // 3. activations and residual rows: sc1 loads (bytes this launch may have written)
-  if (act) {
-    const int r0 = min(arow, M - 1), r1 = min(16 + arow, M - 1), akoff = 8 * (lane >> 4);
-    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)p.x, 0, 0x7fffffff, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < KTM; ++u) {
-      const int k = min(kt0 + u, ktl) * 32 + akoff;
-      a0[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)((r0 * p.ldx + k) * 2), 0, KW_CH_XLD));
-      a1[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)((r1 * p.ldx + k) * 2), 0, KW_CH_XLD));
-    }
-  }
-  if constexpr (EPI == KW_EPI_RESID) {
-    if (wave == 0) {
-#pragma unroll
-      for (int c = 0; c < NCB; ++c) {
-        const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = min(16 * hh + 4 * (lane >> 4) + r, M - 1);
-            hold[c][hh][r] = ld_sc1(p.h + (int64_t)m * p.ldh + n);
-          }
-      }
-    }
-  }
-
-  // 4. MFMA over this wave's k-tiles; LayerNorm statistics on the matrix cores (dec_linear_kernel 2-3)
-  f32x4 c0[NCB], c1[NCB];
-#pragma unroll
-  for (int c = 0; c < NCB; ++c) {
-    c0[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    c1[c] = c0[c];
-  }
-  if (act) {
-#pragma unroll
-    for (int u = 0; u < KTM; ++u) {
-      if (kt0 + u < kt1) {
-#pragma unroll
-        for (int c = 0; c < NCB; ++c) {
-          c0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], w[c][u], c0[c], 0, 0, 0);
-          c1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[c][u], c1[c], 0, 0, 0);
-        }
-      }
-    }
-    if constexpr (LNA) {
-      bf16x8 ones;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
-      f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0, q0 = s0, q1 = s0;
-#pragma unroll
-      for (int u = 0; u < KTM; ++u)
-        if (kt0 + u < kt1) {
-          s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], ones, s0, 0, 0, 0);
-          s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], ones, s1, 0, 0, 0);
-          q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], a0[u], q0, 0, 0, 0);
-          q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], a1[u], q1, 0, 0, 0);
-        }
-      if ((lane & 15) == 0) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          rpart[wave][4 * (lane >> 4) + i][0] = s0[i];
-          rpart[wave][16 + 4 * (lane >> 4) + i][0] = s1[i];
-        }
-      }
-      const int di = (lane & 15) - 4 * (lane >> 4);
-      if (di >= 0 && di < 4) {
-        rpart[wave][lane & 15][1] = q0[di];
-        rpart[wave][16 + (lane & 15)][1] = q1[di];
-      }
-    }
-  }
-
-  // 5. reduce the waves' K slices in wave order; wave 0 continues
-  CH_STAMP(2);
-  if (nw > 1 && act) {
-#pragma unroll
-    for (int c = 0; c < NCB; ++c) {
-      red[wave][c][0][lane] = c0[c];
-      red[wave][c][1][lane] = c1[c];
-    }
-  }
-  __syncthreads();
-  if (wave != 0) return;
-  CH_STAMP(3);
-  for (int w2 = 1; w2 < nw; ++w2)
-#pragma unroll
-    for (int c = 0; c < NCB; ++c) {
-      c0[c] += red[w2][c][0][lane];
-      c1[c] += red[w2][c][1][lane];
-    }
-  if constexpr (LNA) {
-    if (lane < 32) {
-      float sx = 0.f, sq = 0.f;
-      for (int w2 = 0; w2 < nw; ++w2) {
-        sx += rpart[w2][lane][0];
-        sq += rpart[w2][lane][1];
-      }
-      const float inv = 1.f / (float)p.K;
-      const float mean = sx * inv;
-      rstat[lane][0] = mean;
-      rstat[lane][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + p.ln_eps);
-    }
-  }
-
-  // 6. K-split seam (dec_linear_kernel step 5); a workgroup that is not the last arriver is done here
-  if (ksn > 1) {
-    float* mine = p.slab + ((int64_t)cg * ksn + ks) * (NCB * 512);
-#pragma unroll
-    for (int c = 0; c < NCB; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        st_sc1(mine + c * 512 + r * 64 + lane, c0[c][r]);
-        st_sc1(mine + c * 512 + 256 + r * 64 + lane, c1[c][r]);
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int last = 0;
-    if (lane == 0) {
-      const int prev = __hip_atomic_fetch_add(p.cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = prev == ksn - 1;
-      if (last) __hip_atomic_store(p.cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    last = __shfl(last, 0, 64);
-    if (!last) {
-      CH_STAMP(4);
-      if (lane == 0) ch_signal(cp, phi, bl);
-      CH_STAMP(5);
-      return;
-    }
-    const float* all = p.slab + (int64_t)cg * ksn * (NCB * 512);
-    float pv[KSMAX][NCB][8];
-#pragma unroll
-    for (int q = 0; q < KSMAX; ++q)
-#pragma unroll
-      for (int c = 0; c < NCB; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          pv[q][c][e] = q < ksn ? ld_sc1(all + q * NCB * 512 + c * 512 + (e >> 2) * 256 + (e & 3) * 64 + lane) : 0.f;
-#pragma unroll
-    for (int c = 0; c < NCB; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float v0 = pv[0][c][r], v1 = pv[0][c][4 + r];
-#pragma unroll
-        for (int q = 1; q < KSMAX; ++q) {
-          v0 += pv[q][c][r];
-          v1 += pv[q][c][4 + r];
-        }
-        c0[c][r] = v0;
-        c1[c][r] = v1;
-      }
-  }
-
-  // 7. epilogue (dec_linear_kernel step 6) with write-through stores: f32 one word per element, bf16 as
-  //    column pairs (lane n even stores rows r = 0, 1 of columns n, n+1; its odd partner rows 2, 3; the
-  //    partner's values by DPP lane^1).  Every value is formed before the first store: a store's data
-  //    register reused by a later value costs a vmcnt(0) wait per store.
-  const bool even = (lane & 1) == 0;
-  float vals[NCB][2][4];
-  uint32_t pk[NCB][2][2];
-#pragma unroll
-  for (int c = 0; c < NCB; ++c) {
-    const int n = (cg * NCB + c) * 16 + (lane & 15);
-    const float bn = ebias[c];
-    const float cs = ecsum[c];
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * hh + 4 * (lane >> 4) + r;
-        float v = hh ? c1[c][r] : c0[c][r];
-        if constexpr (LNA) v = rstat[m][1] * (v - rstat[m][0] * cs);
-        v += bn;
-        if constexpr (EPI == KW_EPI_RESID) {
-          v += hold[c][hh][r];
-        } else {
-          if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
-          if (n < p.scale_cols) v *= p.scale;
-        }
-        vals[c][hh][r] = v;
-      }
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const float g0 = kw_dpp<0xB1>(even ? vals[c][hh][2] : vals[c][hh][0]);
-      const float g1 = kw_dpp<0xB1>(even ? vals[c][hh][3] : vals[c][hh][1]);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float mine = even ? vals[c][hh][j] : vals[c][hh][2 + j];
-        const float other = j ? g1 : g0;
-        pk[c][hh][j] = even ? pack_bf16x2(mine, other) : pack_bf16x2(other, mine);
-      }
-    }
-  }
-  // stores as buffer stores: per-lane byte offset in one VGPR, the (hh, r) row step in an SGPR (no address
-  // registers to recycle between stores); the packed pairs pinned live first (else each is formed in the
-  // register the previous store is still reading)
-#pragma unroll
-  for (int c = 0; c < NCB; ++c) asm volatile("" : "+v"(pk[c][0][0]), "+v"(pk[c][0][1]), "+v"(pk[c][1][0]), "+v"(pk[c][1][1]));
-  const int rb = 4 * (lane >> 4);
-#pragma unroll
-  for (int c = 0; c < NCB; ++c) {
-    const int n = (cg * NCB + c) * 16 + (lane & 15);
-    const bool nvalid = n < p.N;
-    if constexpr (EPI == KW_EPI_RESID || sizeof(TC) == 4) {
-      float* dst = EPI == KW_EPI_RESID ? p.h : reinterpret_cast<float*>(p.C);
-      const int ld = (int)(EPI == KW_EPI_RESID ? p.ldh : p.ldc);
-      const __amdgpu_buffer_rsrc_t r32 = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
-      const int voff = (rb * ld + n) * 4;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (nvalid && 16 * hh + rb + r < M)
-            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(vals[c][hh][r]), r32, voff, (16 * hh + r) * ld * 4, 16);
-    }
-    if constexpr (EPI == KW_EPI_RESID || sizeof(TC) == 2) {
-      void* dst = EPI == KW_EPI_RESID ? (void*)p.hb : p.C;
-      const int ld = (int)(EPI == KW_EPI_RESID ? p.ldh : p.ldc);
-      const __amdgpu_buffer_rsrc_t r16 = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
-      const int rp = rb + (even ? 0 : 2);
-      const int voff = (rp * ld + (n & ~1)) * 2;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          if ((n & ~1) < p.N && 16 * hh + rp + j < M)
-            __builtin_amdgcn_raw_buffer_store_b32(pk[c][hh][j], r16, voff, (16 * hh + j) * ld * 2, 16);
-    }
-  }
-  CH_STAMP(4);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) ch_signal(cp, phi, bl);
-  CH_STAMP(5);
-}
-
-struct ChNone {};
-
-template <class C0, class C1, class C2>
-__global__ __launch_bounds__(512) void dec_chain_kernel(ChainP cp) {
-  __shared__ f32x4 red[MAXW][2][2][64];
-  __shared__ float rpart[MAXW][32][2];
-  __shared__ float rstat[32][2];
-  const int b = blockIdx.x;
-  if (b < cp.ph[1].off) {
-    ch_phase<C0>(cp, 0, b, red, rpart, rstat);
-  } else if constexpr (std::is_same<C2, ChNone>::value) {
-    ch_phase<C1>(cp, 1, b - cp.ph[1].off, red, rpart, rstat);
-  } else {
-    if (b < cp.ph[2].off)
-      ch_phase<C1>(cp, 1, b - cp.ph[1].off, red, rpart, rstat);
-    else
-      ch_phase<C2>(cp, 2, b - cp.ph[2].off, red, rpart, rstat);
-  }
-}
-
 // LM head over 33..LMR_MAXROWS rows (beam rows: 64 items x 5 beams = 320) as a GEMM: workgroup = 64
 // columns (one 16-column block per wave, all of K) x ALL rows.  Per k-tile the workgroup stages the
 // rows' 32-wide activation slice in LDS once (LDS-DMA, double-buffered, XOR-swizzled for conflict-free
@@ -1247,26 +842,20 @@ Geo choose(int64_t N, int64_t K) {
 #ifdef KW_LAB_OVERRIDES
   // lab builds only (make EXTRA=-DKW_LAB_OVERRIDES OUT=...; tools/lab/*_sweep.sh): KW_DECLIN_GEO="N,K,ncb,ktm,ks"
   // overrides one matrix shape's geometry; read once, thread-safe (function-local static)
-  // (several shapes: entries separated by ';')
-  static const std::array<std::array<int, 5>, 4> lab = [] {
-    std::array<std::array<int, 5>, 4> v{};
+  static const std::array<int, 5> lab = [] {
+    std::array<int, 5> v{0, 0, 0, 0, 0};
     if (const char* e = getenv("KW_DECLIN_GEO")) {
-      int i = 0;
-      for (const char* q = e; q && *q && i < 4; ++i) {
-        sscanf(q, "%d,%d,%d,%d,%d", &v[i][0], &v[i][1], &v[i][2], &v[i][3], &v[i][4]);
-        q = strchr(q, ';');
-        if (q) ++q;
-      }
+      sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
       fprintf(stderr, "kwhisper: lab geometry override KW_DECLIN_GEO=%s\n", e);
     }
     return v;
   }();
-  for (const auto& l : lab)
-    if (l[0] == N && l[1] == K && (l[2] == 1 || l[2] == 2) && (l[3] == 5 || l[3] == 10) && l[4] >= 1 && l[4] <= KSMAX) {
-      g.ncb = l[2];
-      g.ktm = l[3];
-      g.ks = l[4];
-    }
+  if (lab[0] == N && lab[1] == K && (lab[2] == 1 || lab[2] == 2) && (lab[3] == 5 || lab[3] == 10) && lab[4] >= 1 &&
+      lab[4] <= KSMAX) {
+    g.ncb = lab[2];
+    g.ktm = lab[3];
+    g.ks = lab[4];
+  }
 #endif
   const int per_wg = (nkt + g.ks - 1) / g.ks;
   g.nw = (per_wg + g.ktm - 1) / g.ktm;
@@ -1452,172 +1041,6 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     hipError_t e = launch(p, a->epilogue == KW_EPI_RESID, g, a->c_dtype == KW_DT_F32, s);
     if (e != hipSuccess) return kw_set_error(e);
   }
-  return KW_OK;
-}
-
-// ---- chained decode linears (host) -----------------------------------------------------------------------
-namespace {
-
-typedef ChCfg<5, 1, false, KW_EPI_RESID, float> ChR5;   // o / cross-o (K <= 1280)
-typedef ChCfg<5, 1, true, KW_EPI_STORE, bf16_t> ChL5;   // cross q; fc1 of narrow models
-typedef ChCfg<5, 2, true, KW_EPI_STORE, bf16_t> ChL5w;  // fc1 (N >= 5120: two column blocks per workgroup)
-typedef ChCfg<10, 1, false, KW_EPI_RESID, float> ChR10; // fc2 (long K)
-
-// a phase's template signature: k-tiles per wave, column blocks, LayerNorm, epilogue, 16-bit C
-struct ChSig {
-  int ktm, ncb, ln, epi, c16;
-  bool operator==(const ChSig& o) const {
-    return ktm == o.ktm && ncb == o.ncb && ln == o.ln && epi == o.epi && c16 == o.c16;
-  }
-};
-template <class CF>
-ChSig sig_of() {
-  return ChSig{CF::KTM, CF::NCB, CF::LNA ? 1 : 0, CF::EPI, sizeof(typename CF::TC) == 2 ? 1 : 0};
-}
-
-enum { CHAIN_BAD = -1, CHAIN_O_XQ = 0, CHAIN_MLP = 1, CHAIN_MLP_NARROW = 2, CHAIN_MLP_K5 = 3, CHAIN_MLP_NARROW_K5 = 4 };
-
-// which instantiated chain these blocks form (CHAIN_BAD: not one of them / not chainable); fills geos
-int chain_kind(const kw_dec_linear_args* ph, int n, Geo* geos) {
-  if (!ph || n < 2 || n > CH_MAXPH) return CHAIN_BAD;
-  ChSig s[CH_MAXPH];
-  for (int i = 0; i < n; ++i) {
-    const kw_dec_linear_args& a = ph[i];
-    if (!a.x || !a.W || a.M < 1 || a.M > 32 || a.M != ph[0].M || a.N <= 0 || a.N % 32 || a.K <= 0 || a.K % 32 ||
-        a.ldx % 8 || a.ldx < a.K || (uintptr_t)a.x % 16 || a.x_group_cols || a.N > 8192)
-      return CHAIN_BAD;
-    const Geo g = choose(a.N, a.K);
-    const int nkt = (int)(a.K / 32);
-    if ((nkt + g.ks * g.nw - 1) / (g.ks * g.nw) > g.ktm || g.ks > KSMAX || (a.ln && g.ks > 1)) return CHAIN_BAD;
-    if (g.ks > 1 && (!a.workspace || a.ws_bytes < kw_dec_linear_workspace_bytes(a.N, a.K))) return CHAIN_BAD;
-    if (a.epilogue == KW_EPI_RESID) {
-      if (!a.h || !a.hb || a.ldh < a.N || a.ldh % 2 || (uintptr_t)a.hb % 4 || a.ln) return CHAIN_BAD;
-    } else if (a.epilogue == KW_EPI_STORE) {
-      if (!a.C || a.ldc < a.N || (a.c_dtype != KW_DT_F32 && a.c_dtype != KW_DT_BF16)) return CHAIN_BAD;
-      if (a.c_dtype == KW_DT_BF16 && (a.ldc % 2 || (uintptr_t)a.C % 4)) return CHAIN_BAD;
-      if (a.ln && !a.ln_colsum) return CHAIN_BAD;
-    } else {
-      return CHAIN_BAD;
-    }
-    geos[i] = g;
-    s[i] = ChSig{g.ktm, g.ncb, a.ln ? 1 : 0, a.epilogue, a.epilogue == KW_EPI_STORE && a.c_dtype == KW_DT_BF16 ? 1 : 0};
-  }
-  if (n == 2 && s[0] == sig_of<ChR5>() && s[1] == sig_of<ChL5>()) return CHAIN_O_XQ;
-  if (n == 3 && s[0] == sig_of<ChR5>() && s[2] == sig_of<ChR10>()) {
-    if (s[1] == sig_of<ChL5w>()) return CHAIN_MLP;
-    if (s[1] == sig_of<ChL5>()) return CHAIN_MLP_NARROW;
-  }
-  if (n == 3 && s[0] == sig_of<ChR5>() && s[2] == sig_of<ChR5>()) {
-    if (s[1] == sig_of<ChL5w>()) return CHAIN_MLP_K5;
-    if (s[1] == sig_of<ChL5>()) return CHAIN_MLP_NARROW_K5;
-  }
-  return CHAIN_BAD;
-}
-
-constexpr size_t CH_SYNC_BYTES = (size_t)(CH_MAXPH * CH_SHARDS + 2) * CH_LINE * sizeof(int);
-
-#ifdef KW_CH_STAMPS
-unsigned long long* g_stamps = nullptr;
-int g_stamp_wgs = 0;
-unsigned long long* ch_lab_stamps(int wgs) {
-  if (!g_stamps) hipMalloc(&g_stamps, (size_t)4096 * 8 * sizeof(unsigned long long));
-  g_stamp_wgs = wgs;
-  return wgs <= 4096 ? g_stamps : nullptr;
-}
-#endif
-
-}  // namespace
-
-#ifdef KW_CH_STAMPS
-// lab: copy the last chain launch's stamps ([wgs][8] s_memrealtime ticks, 100 MHz) to host; returns wgs
-extern "C" int kw_lab_chain_stamps(unsigned long long* host, int max_wgs) {
-  hipDeviceSynchronize();
-  const int n = std::min(g_stamp_wgs, max_wgs);
-  if (g_stamps && n > 0) hipMemcpy(host, g_stamps, (size_t)n * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
-  return n;
-}
-#endif
-
-extern "C" size_t kw_dec_chain_sync_bytes(void) { return CH_SYNC_BYTES; }
-
-extern "C" int kw_dec_chain_supported(const kw_dec_linear_args* phases, int n_phases) {
-  Geo g[CH_MAXPH];
-  return chain_kind(phases, n_phases, g) != CHAIN_BAD ? 1 : 0;
-}
-
-extern "C" int kw_dec_chain(const kw_dec_linear_args* phases, int n_phases, void* sync, size_t sync_bytes,
-                            kw_stream_t stream) {
-  Geo geo[CH_MAXPH];
-  const int kind = chain_kind(phases, n_phases, geo);
-  if (kind == CHAIN_BAD)
-    return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_chain: not a supported chain (see kw_dec_chain_supported)");
-  if (!sync || sync_bytes < CH_SYNC_BYTES || (uintptr_t)sync % 128)
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_chain: needs a zero-filled, 128-B aligned sync area of kw_dec_chain_sync_bytes()");
-  ChainP cp{};
-  cp.nph = n_phases;
-  cp.sync = reinterpret_cast<int*>(sync);
-  int off = 0, nwmax = 1;
-  for (int i = 0; i < n_phases; ++i) {
-    const kw_dec_linear_args& a = phases[i];
-    const Geo& g = geo[i];
-    DecP& p = cp.ph[i].p;
-    p = DecP{};
-    p.x = reinterpret_cast<const bf16_t*>(a.x);
-    p.ldx = a.ldx;
-    p.ln = a.ln;
-    p.ln_eps = a.ln_eps;
-    p.ln_colsum = a.ln_colsum;
-    p.W = reinterpret_cast<const bf16x8*>(a.W);
-    p.bias = a.bias;
-    p.C = a.C;
-    p.ldc = a.ldc;
-    p.gelu = a.gelu;
-    p.scale = a.scale;
-    p.scale_cols = (int)a.scale_cols;
-    p.h = a.h;
-    p.hb = reinterpret_cast<bf16_t*>(a.hb);
-    p.ldh = a.ldh;
-    p.M = (int)a.M;
-    p.N = (int)a.N;
-    p.K = (int)a.K;
-    p.cnt = reinterpret_cast<int*>(a.workspace);
-    p.slab = a.workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(a.workspace) + CNT_MAX * sizeof(int)) : nullptr;
-    ChainPh& c = cp.ph[i];
-    c.ksn = g.ks;
-    c.ncg = (int)((a.N + 16 * g.ncb - 1) / (16 * g.ncb));
-    c.nwg = c.ncg * g.ks;
-    c.off = off;
-    c.nw = g.nw;
-    off += c.nwg;
-    nwmax = std::max(nwmax, g.nw);
-  }
-  for (int i = n_phases; i < CH_MAXPH; ++i) cp.ph[i].off = off;
-#ifdef KW_CH_STAMPS
-  cp.stamps = ch_lab_stamps(off);
-#endif
-  hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)off), block((unsigned)(64 * nwmax));
-  switch (kind) {
-    case CHAIN_O_XQ: hipLaunchKernelGGL((dec_chain_kernel<ChR5, ChL5, ChNone>), grid, block, 0, s, cp); break;
-    case CHAIN_MLP: hipLaunchKernelGGL((dec_chain_kernel<ChR5, ChL5w, ChR10>), grid, block, 0, s, cp); break;
-    case CHAIN_MLP_K5: hipLaunchKernelGGL((dec_chain_kernel<ChR5, ChL5w, ChR5>), grid, block, 0, s, cp); break;
-    case CHAIN_MLP_NARROW_K5: hipLaunchKernelGGL((dec_chain_kernel<ChR5, ChL5, ChR5>), grid, block, 0, s, cp); break;
-    default: hipLaunchKernelGGL((dec_chain_kernel<ChR5, ChL5, ChR10>), grid, block, 0, s, cp); break;
-  }
-  KW_CHECK_LAUNCH();
-  return KW_OK;
-}
-
-extern "C" int kw_dec_chain_status(void* sync, int* flagged, kw_stream_t stream) {
-  if (!sync || !flagged) return kw_set_error_msg(KW_EINVAL, "kw_dec_chain_status: null sync area or output");
-  int* err = reinterpret_cast<int*>(sync) + (CH_MAXPH * CH_SHARDS + 1) * CH_LINE;
-  int v = 0;
-  hipStream_t s = (hipStream_t)stream;
-  hipError_t e = hipMemcpyAsync(&v, err, sizeof(int), hipMemcpyDeviceToHost, s);
-  if (e == hipSuccess) e = hipStreamSynchronize(s);
-  if (e == hipSuccess && v) e = hipMemsetAsync(err, 0, sizeof(int), s);
-  if (e != hipSuccess) return kw_set_error(e);
-  *flagged = v;
   return KW_OK;
 }
 

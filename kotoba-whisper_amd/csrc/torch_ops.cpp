@@ -116,13 +116,14 @@ void gemm(const Tensor& A, const Tensor& W, const optional<Tensor>& bias, Tensor
 
 // ---- decode-step linear over packed weights -----------------------------------------------------------
 // geo = [x_offset, ldx, ln, c_offset, ldc, gelu, scale_cols, resid_row0, ldh, M, N, K, x_group_cols, x_group_stride]
-kw_dec_linear_args dec_args(const Tensor& x, const Tensor& W, const optional<Tensor>& bias,
-                            const optional<Tensor>& ln_colsum, const optional<Tensor>& C, const optional<Tensor>& h,
-                            const optional<Tensor>& hb, const Tensor& workspace, const int64_t* geo, double ln_eps,
-                            double scale, const char* w) {
+void dec_linear(const Tensor& x, const Tensor& W, const optional<Tensor>& bias, const optional<Tensor>& ln_colsum,
+                optional<Tensor> C, optional<Tensor> h, optional<Tensor> hb, Tensor& workspace,
+                std::vector<int64_t> geo, double ln_eps, double scale) {
+  const char* w = "kw_dec_linear";
   dev(x, w), dev(W, w), dev(bias, w), dev(ln_colsum, w), dev(C, w), dev(h, w), dev(hb, w), dev(workspace, w);
+  TORCH_CHECK_VALUE(geo.size() == 14, "kw_dec_linear: geo must hold 14 integers");
   TORCH_CHECK_VALUE(x.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16,
-                    w, " takes bf16 activations and packed bf16 weights");
+                    "kw_dec_linear takes bf16 activations and packed bf16 weights");
   kw_dec_linear_args a{};
   a.x = ptr(x, geo[0]);
   a.ldx = geo[1];
@@ -152,35 +153,8 @@ kw_dec_linear_args dec_args(const Tensor& x, const Tensor& W, const optional<Ten
   a.x_group_cols = geo[12], a.x_group_stride = geo[13];
   a.workspace = ptr(workspace);
   a.ws_bytes = (size_t)workspace.numel() * workspace.element_size();
-  return a;
-}
-
-void dec_linear(const Tensor& x, const Tensor& W, const optional<Tensor>& bias, const optional<Tensor>& ln_colsum,
-                optional<Tensor> C, optional<Tensor> h, optional<Tensor> hb, Tensor& workspace,
-                std::vector<int64_t> geo, double ln_eps, double scale) {
-  const char* w = "kw_dec_linear";
-  TORCH_CHECK_VALUE(geo.size() == 14, "kw_dec_linear: geo must hold 14 integers");
-  const kw_dec_linear_args a = dec_args(x, W, bias, ln_colsum, C, h, hb, workspace, geo.data(), ln_eps, scale, w);
   c10::DeviceGuard g(W.device());
   check(kw_dec_linear(&a, stream_of(W)), w);
-}
-
-// Chained linears (kw_dec_chain): per phase the 8 tensors of dec_linear (x, W, bias, ln_colsum, C, h, hb,
-// workspace; absent = None), its 14 geo integers and (ln_eps, scale).
-void dec_chain(const std::vector<optional<Tensor>>& t, std::vector<int64_t> geo, std::vector<double> f, Tensor& sync) {
-  const char* w = "kw_dec_chain";
-  const size_t n = t.size() / 8;
-  TORCH_CHECK_VALUE(n >= 2 && n <= 3 && t.size() == 8 * n && geo.size() == 14 * n && f.size() == 2 * n,
-                    "kw_dec_chain: 2-3 phases of 8 tensors, 14 geo integers and 2 floats each");
-  dev(sync, w);
-  kw_dec_linear_args a[3];
-  for (size_t i = 0; i < n; ++i) {
-    const optional<Tensor>* q = &t[8 * i];
-    TORCH_CHECK_VALUE(q[0].has_value() && q[1].has_value() && q[7].has_value(), "kw_dec_chain: x, W and workspace are required");
-    a[i] = dec_args(*q[0], *q[1], q[2], q[3], q[4], q[5], q[6], *q[7], geo.data() + 14 * i, f[2 * i], f[2 * i + 1], w);
-  }
-  c10::DeviceGuard g(sync.device());
-  check(kw_dec_chain(a, (int)n, ptr(sync), (size_t)sync.numel() * sync.element_size(), stream_of(sync)), w);
 }
 
 void pack_weight(const Tensor& W, Tensor& out) {
@@ -372,7 +346,6 @@ void beam_select(const Tensor& cand_val, const Tensor& cand_idx, Tensor& ids, op
 int64_t workspace_bytes(std::string kind, std::vector<int64_t> d) {
   auto n = [&](size_t i) { return at_(d, i, "kw::workspace_bytes"); };
   if (kind == "dec_linear") return (int64_t)kw_dec_linear_workspace_bytes(n(0), n(1));
-  if (kind == "dec_chain_sync") return (int64_t)kw_dec_chain_sync_bytes();
   if (kind == "packed_weight") return (int64_t)kw_packed_weight_bytes(n(0), n(1));
   if (kind == "self_attn") return (int64_t)kw_self_attn_workspace(n(0), n(1), n(2));
   if (kind == "cross_attn") return (int64_t)kw_cross_attn_workspace(n(0), n(1), n(2), n(3), n(4));
@@ -394,7 +367,6 @@ TORCH_LIBRARY(kw, m) {
   m.def("gemm(Tensor A, Tensor W, Tensor? bias, Tensor(a!) C, Tensor? row_add, int[] geo, float scale, int dtype) -> ()");
   m.def("dec_linear(Tensor x, Tensor W, Tensor? bias, Tensor? ln_colsum, Tensor(a!)? C, Tensor(b!)? h, "
         "Tensor(c!)? hb, Tensor(d!) workspace, int[] geo, float ln_eps, float scale) -> ()");
-  m.def("dec_chain(Tensor(a!)?[] tensors, int[] geo, float[] f, Tensor(b!) sync) -> ()");
   m.def("pack_weight(Tensor W, Tensor(a!) out) -> ()");
   m.def("layernorm(Tensor(a!) x, Tensor gamma, Tensor beta, float eps, Tensor(b!) y, Tensor? delta) -> ()");
   m.def("attention(Tensor qkv, int B, int H, int T, int hd, Tensor(a!) out) -> ()");
@@ -422,7 +394,6 @@ TORCH_LIBRARY_IMPL(kw, CUDA, m) {
   m.impl("mel_to_time_major", &mel_to_time_major);
   m.impl("gemm", &gemm);
   m.impl("dec_linear", &dec_linear);
-  m.impl("dec_chain", &dec_chain);
   m.impl("pack_weight", &pack_weight);
   m.impl("layernorm", &layernorm);
   m.impl("attention", &attention);

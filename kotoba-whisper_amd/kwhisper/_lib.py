@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("KWHISPER_LIB") or os.path.join(os.path.dirname(os.pat
 # torch.ops.kw.* (csrc/torch_ops.cpp), linked against libkwhisper.so found beside it
 TORCH_LIB_PATH = os.environ.get("KWHISPER_TORCH_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                       "libkwhisper_torch.so")
-TORCH_OPS = ("log_mel", "mel_to_time_major", "gemm", "dec_linear", "dec_chain", "pack_weight", "layernorm", "attention", "embed",
+TORCH_OPS = ("log_mel", "mel_to_time_major", "gemm", "dec_linear", "pack_weight", "layernorm", "attention", "embed",
              "self_attn_step", "cross_attn_step", "cross_attn_enc", "greedy_step", "beam_logprobs", "beam_select")
 
 KW_OK, KW_EINVAL, KW_EHIP, KW_EUNSUPPORTED = 0, 1, 2, 3
@@ -102,10 +102,6 @@ EXPORTS = {
     "kw_gemm": (ctypes.c_int, [ctypes.POINTER(GemmArgs), c_vp]),
     "kw_dec_linear": (ctypes.c_int, [ctypes.POINTER(DecLinearArgs), c_vp]),
     "kw_dec_linear_workspace_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
-    "kw_dec_chain": (ctypes.c_int, [ctypes.POINTER(DecLinearArgs), ctypes.c_int, c_vp, ctypes.c_size_t, c_vp]),
-    "kw_dec_chain_supported": (ctypes.c_int, [ctypes.POINTER(DecLinearArgs), ctypes.c_int]),
-    "kw_dec_chain_sync_bytes": (ctypes.c_size_t, []),
-    "kw_dec_chain_status": (ctypes.c_int, [c_vp, ctypes.POINTER(ctypes.c_int), c_vp]),
     "kw_pack_weight": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp]),
     "kw_packed_weight_bytes": (ctypes.c_size_t, [c_i64, c_i64]),
     "kw_layernorm": (ctypes.c_int, [c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_float, c_vp, ctypes.c_int, c_vp, c_vp]),

@@ -54,7 +54,6 @@ class DecodeSession:
         self.logits = torch.empty((R, s.vocab_size), device=dev, dtype=torch.float32)
         self._bufs = {}
         self._plans = {}
-        self.chain_sync = None  # kw_dec_chain counters (created with the first chained plan)
         # split-K seam scratch shared by every decode linear of a step (stream-ordered; zeroed once)
         ws = 0
         if eng.packed:
@@ -157,8 +156,6 @@ class DecodeSession:
             # final LayerNorm (folded into the packed LM head) + proj_out on the last position of every row
             seq.append(lin(hb, eng.lm_w, B, s.vocab_size, d, ldx=q * d, x_offset=(q - 1) * d,
                            ln=(eps, eng.lm_cs), bias=eng.lm_b, C=self.logits, workspace=ws, tag="lm_head"))
-            if eng.chain_linears:
-                seq = self._chained(seq)
             self._plans[q] = seq
             return seq
         seq = [("embed", q, b["h"])]
@@ -182,28 +179,6 @@ class DecodeSession:
         seq += self._gemm(b["x"], eng.lm_w, self.logits, B, s.vocab_size, d, lda=q * d, a_offset=(q - 1) * d)
         self._plans[q] = seq
         return seq
-
-    _CHAINS = (("o", "xq"), ("xo", "fc1", "fc2"))
-
-    def _chained(self, seq):
-        """Replace each run of linears that feed each other (o -> xq, xo -> fc1 -> fc2) by one kw_dec_chain
-        launch where the kernel supports the shapes (M <= 32 rows: the single-token step of up to 32 rows)."""
-        out, i = [], 0
-        while i < len(seq):
-            for tags in self._CHAINS:
-                run = seq[i:i + len(tags)]
-                if (len(run) == len(tags) and all(getattr(p, "tag", None) == t for p, t in zip(run, tags))
-                        and ops.dec_chain_supported(run)):
-                    if self.chain_sync is None:
-                        self.chain_sync = torch.zeros(((ops.dec_chain_sync_bytes() + 3) // 4,), device=self.eng.device,
-                                                      dtype=torch.int32)
-                    out.append(ops.DecChainPlan(run, self.chain_sync, tag="+".join(tags)))
-                    i += len(tags)
-                    break
-            else:
-                out.append(seq[i])
-                i += 1
-        return out
 
     def _run(self, seq):
         eng, s = self.eng, self.eng.shape

@@ -69,9 +69,6 @@ class WhisperEngine:
         if cross_attention not in ("kv_cache", "encoder_output"):
             raise ValueError("cross_attention must be 'kv_cache' or 'encoder_output'")
         self.cross_attention = cross_attention
-        # decode linears that feed each other within a layer (o -> cross q, cross o -> fc1 -> fc2) run as one
-        # kw_dec_chain launch where it supports the shapes (bitwise the same results); False = one launch each
-        self.chain_linears = False
         L.load()
         L.load_torch_ops()  # torch.ops.kw.* (the launch path of every op); raises if it was not built
         self.shape = shape

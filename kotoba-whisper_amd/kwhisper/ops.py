@@ -72,8 +72,7 @@ def _ws_bytes(kind: str, *dims) -> int:
     fn = {"dec_linear": "kw_dec_linear_workspace_bytes", "packed_weight": "kw_packed_weight_bytes",
           "self_attn": "kw_self_attn_workspace", "cross_attn": "kw_cross_attn_workspace",
           "cross_attn_enc": "kw_cross_attn_enc_workspace",
-          "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace",
-          "dec_chain_sync": "kw_dec_chain_sync_bytes"}[kind]
+          "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace"}[kind]
     return int(getattr(_lib(), fn)(*dims))
 
 
@@ -267,60 +266,6 @@ class DecLinearPlan:
             _kw().dec_linear(*self._targs)
         else:
             L.check(_lib().kw_dec_linear(self._ref, _s()), "kw_dec_linear")
-
-
-def dec_chain_sync_bytes() -> int:
-    return _ws_bytes("dec_chain_sync")
-
-
-def dec_chain_supported(plans) -> bool:
-    """Whether ``kw_dec_chain`` takes these ``DecLinearPlan``s as one launch (phase i reading phase i-1's output)."""
-    if not 2 <= len(plans) <= 3 or not all(isinstance(p, DecLinearPlan) for p in plans):
-        return False
-    arr = (L.DecLinearArgs * len(plans))(*[p.args for p in plans])
-    return bool(_lib().kw_dec_chain_supported(arr, len(plans)))
-
-
-class DecChainPlan:
-    """Consecutive dependent ``DecLinearPlan``s as ONE ``kw_dec_chain`` launch: results bitwise those of calling
-    the plans in turn; each phase's weight stream starts before the phase whose output it reads has finished.
-    ``sync``: a zero-filled device tensor of >= dec_chain_sync_bytes() bytes (launches leave it zeroed); one
-    serves every chain on a stream."""
-
-    def __init__(self, plans, sync: torch.Tensor, tag=None):
-        plans = list(plans)
-        _cuda(sync)
-        if not dec_chain_supported(plans):
-            raise ValueError("kw_dec_chain: these linears do not form a supported chain")
-        nbytes = sync.numel() * sync.element_size()
-        if nbytes < dec_chain_sync_bytes():
-            raise ValueError("kw_dec_chain: sync area too small")
-        self.tag = tag
-        self.plans = plans
-        self._arr = (L.DecLinearArgs * len(plans))(*[p.args for p in plans])
-        tens, geo, f = [], [], []
-        for p in plans:
-            x, W, bias, colsum, C, h, hb, ws, g, eps, scale = p._targs
-            tens += [x, W, bias, colsum, C, h, hb, ws]
-            geo += g
-            f += [eps, scale]
-        self._targs = (tens, geo, f, sync)
-        self._sync = (ctypes.c_void_p(sync.data_ptr()), nbytes)
-        self._keep = (tuple(p._keep for p in plans), sync)
-
-    def __call__(self):
-        if _BACKEND == "torch":
-            _kw().dec_chain(*self._targs)
-        else:
-            L.check(_lib().kw_dec_chain(self._arr, len(self.plans), self._sync[0], self._sync[1], _s()), "kw_dec_chain")
-
-
-def dec_chain_status(sync: torch.Tensor) -> int:
-    """Sync the stream and return (and clear) the chain sync area's error word: nonzero = a chained phase waited
-    past its bound (its results are wrong)."""
-    flag = ctypes.c_int(0)
-    L.check(_lib().kw_dec_chain_status(ctypes.c_void_p(sync.data_ptr()), ctypes.byref(flag), _s()), "kw_dec_chain_status")
-    return int(flag.value)
 
 
 def ln_colsum(W: torch.Tensor) -> torch.Tensor:
