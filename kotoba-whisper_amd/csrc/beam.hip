@@ -79,6 +79,37 @@ __device__ __forceinline__ uint64_t wave_max_u64(uint64_t k) {
   return u64_max_swap32(u64_max_swap16(k));
 }
 
+// The wave's best key, exactly wave_max_u64(k), at about a third of its VALU: a 32-bit maximum of the keys'
+// value words (one v_max_u32 per DPP / swap step instead of a 64-bit compare and two selects), a ballot of the
+// lanes that hold it, and the holder's key by readlane; only a tie on the value (several lanes, one value)
+// falls back to the 64-bit maximum over those lanes (the lowest token among them).  Value words are never 0
+// for a key (bkey's monotonic bits of any non-NaN score are >= 0x007FFFFF); key 0 = no candidate.
+template <int CTRL>
+__device__ __forceinline__ uint32_t u32_max_dpp(uint32_t v) {
+  const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+  return o > v ? o : v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+  v = u32_max_dpp<0xB1>(v);
+  v = u32_max_dpp<0x4E>(v);
+  v = u32_max_dpp<0x141>(v);
+  v = u32_max_dpp<0x140>(v);
+  const auto a = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  v = a[0] > a[1] ? a[0] : a[1];
+  const auto b = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return b[0] > b[1] ? b[0] : b[1];
+}
+__device__ __forceinline__ uint64_t wave_best_key(uint64_t k) {
+  const uint32_t hi = (uint32_t)(k >> 32);
+  const uint32_t gh = wave_max_u32(hi);
+  const uint64_t hit = __ballot(hi == gh && gh != 0);
+  if (hit == 0) return 0;
+  if (hit & (hit - 1)) return wave_max_u64(hi == gh ? k : 0);
+  const int w = __builtin_ctzll(hit);
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, w) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k, w);
+}
+
 __global__ __launch_bounds__(ST) void beam_logprobs_kernel(kw_beam_logprobs_args a) {
   __shared__ float shf[ST / 64];
   __shared__ int shi[ST / 64][2];
@@ -378,7 +409,7 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
     };
     fill();
     for (int j = 0; j < kp; ++j) {
-      const uint64_t g = wave_max_u64(c0);
+      const uint64_t g = wave_best_key(c0);
       if (lane == 0) wck[list][wv][j] = g;
       bool need = false;
       if (g != 0 && c0 == g) {
@@ -410,7 +441,7 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
         if (e < n) bins3(wck[list][e / kp][e % kp], c0, c1, c2);
       }
       for (int j = 0; j < kp; ++j) {
-        const uint64_t g = wave_max_u64(c0);
+        const uint64_t g = wave_best_key(c0);
         if (g != 0 && c0 == g) { c0 = c1; c1 = c2; c2 = 0; }
         if (lane == 0) {
           pub[9 + list * 2 * KP + 2 * j] = g ? bkey_val(g) : -INFINITY;
@@ -506,7 +537,7 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
   for (int j = 0; j < K; ++j) {
     uint64_t b = kk[0] > kk[1] ? kk[0] : kk[1];
     b = b > kk[2] ? b : kk[2];
-    const uint64_t g = wave_max_u64(b);
+    const uint64_t g = wave_best_key(b);
     if (g == 0) {  // no candidate left (cannot happen with a sane config): as the reference's -inf / 0
       if (lane == 0) {
         a.cand_val[(int64_t)r * K + j] = -INFINITY;
