@@ -418,29 +418,32 @@ __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, 
   const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
   Row8<T> kr[8], vr[8];
   // key groups j past the chunk (k0 + 32j >= k1: workgroup-uniform, e.g. the short self-attention chunks of
-  // early decode steps) load nothing and hold zeros (their scores are masked, p = 0)
+  // early decode steps) load nothing, and every use of their registers sits behind the same uniform test
+  // (no zero fill: a phi of loaded and zeroed registers made the compiler copy a pending load register and
+  // wait vmcnt(0) after the second row load).  kp(k, j) / vp(k, j) must not load either: an address that
+  // waits on a load costs a vmcnt(0) per row.  Skipped groups contributed p = 0 before: same results.
+  auto act = [&](int j) { return k0 + 32 * j < k1; };
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (k0 + 32 * j < k1) kr[j] = ld_row8<T>(kp(min(k0 + slot + 32 * j, k1 - 1)) + sub * 8);
-    else kr[j] = Row8<T>{};
-  }
+  for (int j = 0; j < 8; ++j)
+    if (act(j)) kr[j] = ld_row8<T>(kp(min(k0 + slot + 32 * j, k1 - 1), j) + sub * 8);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (k0 + 32 * j < k1) vr[j] = ld_row8<T>(vp(min(k0 + slot + 32 * j, k1 - 1)) + sub * 8);
-    else vr[j] = Row8<T>{};
-  }
+  for (int j = 0; j < 8; ++j)
+    if (act(j)) vr[j] = ld_row8<T>(vp(min(k0 + slot + 32 * j, k1 - 1), j) + sub * 8);
   float sc[8];
   float mx = -INFINITY;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    float kv[8];
-    unpack8<T>(kr[j], kv);
-    float sj = 0.f;
+    sc[j] = -INFINITY;
+    if (act(j)) {
+      float kv[8];
+      unpack8<T>(kr[j], kv);
+      float sj = 0.f;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kv[i], sj);
-    sj = kw_sum8(sj);
-    sc[j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
-    mx = fmaxf(mx, sc[j]);
+      for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kv[i], sj);
+      sj = kw_sum8(sj);
+      sc[j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
+      mx = fmaxf(mx, sc[j]);
+    }
   }
   mx = wave_max(mx);
   if (lane == 0) stat[wave] = mx;
@@ -449,12 +452,14 @@ __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, 
   float lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[j] - m) : 0.f;
-    lsum += pj;
-    float vv[8];
-    unpack8<T>(vr[j], vv);
+    if (act(j)) {
+      const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[j] - m) : 0.f;
+      lsum += pj;
+      float vv[8];
+      unpack8<T>(vr[j], vv);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
+    }
   }
   // lanes of one wave with equal sub hold the same dims: reduce over lane bits 3..5
 #pragma unroll
@@ -588,8 +593,8 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q
   float qv[8];
   load8<T>(q + (int64_t)bq * H * HD + h * HD + sub * 8, qv);
   float m, l, o;
-  attend_chunk<T>(qv, k0, k1, [&](int k) { return kb + (int64_t)k * HD; }, [&](int k) { return vb + (int64_t)k * HD; },
-                  red, stat, m, l, o);
+  attend_chunk<T>(qv, k0, k1, [&](int k, int) { return kb + (int64_t)k * HD; },
+                  [&](int k, int) { return vb + (int64_t)k * HD; }, red, stat, m, l, o);
   T* orow = out + (int64_t)bq * H * HD + h * HD;
   if (ns == 1) {
     if (threadIdx.x < HD) TypeIO<T>::st(orow + threadIdx.x, o / l);
@@ -1107,7 +1112,7 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
 // decoder self-attention for one new position (q_len == 1): split 0 appends k/v at L-1; each split
 // attends over its <= 256-key chunk of [0, L) (the new row read from qkv, never from the cache in the
 // same launch); splits beyond L exit; the last arriving split combines.
-template <typename T>
+template <typename T, bool BP>
 __global__ __launch_bounds__(256) void self_attn_step1(const T* __restrict__ qkv, int H, T* __restrict__ kc,
                                                        T* __restrict__ vc, int t_max, const int32_t* __restrict__ cur_len,
                                                        const int32_t* __restrict__ bp, int bp_stride,
@@ -1134,14 +1139,25 @@ __global__ __launch_bounds__(256) void self_attn_step1(const T* __restrict__ qkv
   float qv[8];
   load8<T>(row + sub * 8, qv);
   float m, l, o;
-  // beam search: position k of this row lives in cache row bp[b][k] (a shared prefix), else in row b
-  const int32_t* bpr = bp ? bp + (int64_t)b * bp_stride : nullptr;
-  auto slot = [&](int k) -> int64_t {
-    return ((int64_t)(bpr ? bpr[k] : b) * H + h) * t_max * HD + (int64_t)k * HD;
-  };
-  attend_chunk<T>(qv, k0, min(L, k0 + 256),
-                  [&](int k) -> const T* { return k < p0 ? kc + slot(k) : row + d; },
-                  [&](int k) -> const T* { return k < p0 ? vc + slot(k) : row + 2 * d; }, red, stat, m, l, o);
+  // beam search: position k of this row lives in cache row bp[b][k] (a shared prefix), else in row b.  The
+  // cache rows of this thread's 8 key slots (attend_chunk's k = min(k0 + slot + 32 j, k1 - 1)) are resolved
+  // before any K/V load, so the 16 row loads issue back to back (a slot-table load inside the address of
+  // each row put a vmcnt(0) before every row load, on the greedy path too)
+  const int k1 = min(L, k0 + 256);
+  const int kslot = (tid >> 6) * 8 + ((tid & 63) >> 3);
+  int32_t crow[8];
+  if constexpr (BP) {  // (a separate instantiation: a runtime branch joins with a vmcnt(0) before the K loads)
+    const int32_t* bpr = bp + (int64_t)b * bp_stride;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) crow[j] = bpr[min(k0 + kslot + 32 * j, k1 - 1)];  // < L <= t_max <= bp_stride
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) crow[j] = b;
+  }
+  auto slot = [&](int k, int j) -> int64_t { return ((int64_t)crow[j] * H + h) * t_max * HD + (int64_t)k * HD; };
+  attend_chunk<T>(qv, k0, k1,
+                  [&](int k, int j) -> const T* { return k < p0 ? kc + slot(k, j) : row + d; },
+                  [&](int k, int j) -> const T* { return k < p0 ? vc + slot(k, j) : row + 2 * d; }, red, stat, m, l, o);
   T* orow = out + (int64_t)b * d + h * HD;
   if (ns == 1) {
     if (tid < HD) TypeIO<T>::st(orow + tid, o / l);
@@ -1200,11 +1216,13 @@ extern "C" int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t 
     int* cnt = (int*)((char*)workspace + (size_t)(B * H) * 2 * (HD + 2) * sizeof(float));
     dim3 grid((unsigned)(B * H), (unsigned)((t_max + 255) / 256));
     if (dtype == KW_DT_BF16)
-      hipLaunchKernelGGL(self_attn_step1<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)qkv, (int)H, (bf16_t*)k_cache,
-                         (bf16_t*)v_cache, (int)t_max, cur_len, bp, (int)bp_stride, part, cnt, (bf16_t*)out);
+      hipLaunchKernelGGL((bp ? self_attn_step1<bf16_t, true> : self_attn_step1<bf16_t, false>), grid, dim3(256), 0, s,
+                         (const bf16_t*)qkv, (int)H, (bf16_t*)k_cache, (bf16_t*)v_cache, (int)t_max, cur_len, bp,
+                         (int)bp_stride, part, cnt, (bf16_t*)out);
     else
-      hipLaunchKernelGGL(self_attn_step1<float>, grid, dim3(256), 0, s, (const float*)qkv, (int)H, (float*)k_cache,
-                         (float*)v_cache, (int)t_max, cur_len, bp, (int)bp_stride, part, cnt, (float*)out);
+      hipLaunchKernelGGL((bp ? self_attn_step1<float, true> : self_attn_step1<float, false>), grid, dim3(256), 0, s,
+                         (const float*)qkv, (int)H, (float*)k_cache, (float*)v_cache, (int)t_max, cur_len, bp,
+                         (int)bp_stride, part, cnt, (float*)out);
   } else if (dtype == KW_DT_BF16) {
     hipLaunchKernelGGL(self_attn_step<bf16_t>, dim3((unsigned)(B * H)), dim3(256), 0, s, (const bf16_t*)qkv, (int)q_len,
                        (int)H, (bf16_t*)k_cache, (bf16_t*)v_cache, (int)t_max, cur_len, (bf16_t*)out);

@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--only", default="", help="comma list of kernel names to run (default: all)")
     ap.add_argument("--eager", action="store_true", help="no graph, no timing (for rocprofv3 --pmc passes)")
     ap.add_argument("--warm", action="store_true", help="one weight buffer per linear (L2/MALL-warm replays)")
+    ap.add_argument("--self-t", default="132", help="comma list of self-attention lengths (cur_len) to time")
     a = ap.parse_args()
     global EAGER
     EAGER = a.eager
@@ -127,24 +128,30 @@ def main():
             us = timeit(fns, max(1, a.reps // 4))
             res["xenc"] = {"us": round(us, 2), "GBps": round(B * S * d * 2 / us / 1e3, 1), "note": "same e every launch"}
     # attention kernels
-    if not want("cross_attn") and not want("self_attn_t132"):
+    if not want("cross_attn") and not want("self_attn"):
         print(json.dumps(res))
         return
-    cross = [torch.randn(2, B, H, S, 64, device=dev).bfloat16() for _ in range(nl)]
     q = torch.randn(B, d, device=dev).bfloat16()
     out = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
-    ws = torch.zeros(ops.cross_attn_workspace_bytes(B, 1, H, 64, S) // 4 + 1, device=dev)
-    fns = [lambda c=c: ops.cross_attn_step(q, B, 1, H, 64, c[0], c[1], S, out, ws) for c in cross]
-    us = timeit(fns, max(1, a.reps // 4))
-    res["cross_attn"] = {"us": round(us, 2), "GBps": round(2 * B * H * S * 64 * 2 / us / 1e3, 1)}
-    del cross
+    if want("cross_attn"):
+        cross = [torch.randn(2, B, H, S, 64, device=dev).bfloat16() for _ in range(nl)]
+        ws = torch.zeros(ops.cross_attn_workspace_bytes(B, 1, H, 64, S) // 4 + 1, device=dev)
+        fns = [lambda c=c: ops.cross_attn_step(q, B, 1, H, 64, c[0], c[1], S, out, ws) for c in cross]
+        us = timeit(fns, max(1, a.reps // 4))
+        res["cross_attn"] = {"us": round(us, 2), "GBps": round(2 * B * H * S * 64 * 2 / us / 1e3, 1)}
+        del cross
+    if not want("self_attn"):
+        print(json.dumps(res))
+        return
     kc = torch.randn(nl, B, H, 448, 64, device=dev).bfloat16()
     vc = torch.randn(nl, B, H, 448, 64, device=dev).bfloat16()
     qkv = torch.randn(B, 3 * d, device=dev).bfloat16()
-    cur = torch.tensor([132], dtype=torch.int32, device=dev)
     sws = torch.zeros(ops.self_attn_workspace_bytes(B, H, 448) // 4 + 1, device=dev)
-    fns = [lambda i=i: ops.self_attn_step(qkv, B, 1, H, 64, kc[i], vc[i], 448, cur, out, sws) for i in range(nl)]
-    res["self_attn_t132"] = {"us": round(timeit(fns, a.reps), 2)}
+    for t in [int(x) for x in a.self_t.split(",")]:
+        cur = torch.tensor([t], dtype=torch.int32, device=dev)
+        fns = [lambda i=i, cur=cur: ops.self_attn_step(qkv, B, 1, H, 64, kc[i], vc[i], 448, cur, out, sws)
+               for i in range(nl)]
+        res[f"self_attn_t{t}"] = {"us": round(timeit(fns, a.reps), 2)}
     print(json.dumps(res))
 
 
