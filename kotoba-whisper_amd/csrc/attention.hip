@@ -760,11 +760,23 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
   const int k0 = split * chunk, k1 = min(S, k0 + chunk);
   const T* kb = kc + ((int64_t)b * H + h) * S * HD;
   const T* vb = vc + ((int64_t)b * H + h) * S * HD;
+  // every load in flight before any arithmetic: the group's query rows (clamped to its last row: no branch),
+  // then the chunk's K and V rows; the scheduling barrier keeps the compiler from sinking the V loads below
+  // the first row's scores (which put a vmcnt(0) between the K and V streams and another before each later
+  // row's query load)
+  Row8<T> qr[QN];
+#pragma unroll
+  for (int r = 0; r < QN; ++r) {
+    const T* qp = q + ((int64_t)(b * q_len + qi0 + min(r, nq - 1))) * H * HD + h * HD + sub * 8;
+    qr[r].u[0] = *reinterpret_cast<const u32x4*>(qp);
+    if constexpr (sizeof(T) == 4) qr[r].u[1] = *(reinterpret_cast<const u32x4*>(qp) + 1);
+  }
   Row8<T> kr[8], vr[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) kr[j] = ld_row8<T>(kb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8);
 #pragma unroll
   for (int j = 0; j < 8; ++j) vr[j] = ld_row8<T>(vb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8);
+  __builtin_amdgcn_sched_barrier(0);
   // rows in blocks of 4 (one combine thread per (row, dim) per block): the K/V registers stay live
   // across the blocks, so an item's QN rows cost ONE K/V pass
   float mrow[QN], lrow[QN], orow_acc[QN];
@@ -776,7 +788,7 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
     for (int r = 0; r < 4; ++r) {
       if (r0 + r >= nq) break;  // (uniform: rows past the group's last are neither computed nor read)
       float qv[8];
-      load8<T>(q + ((int64_t)(b * q_len + qi0 + r0 + r)) * H * HD + h * HD + sub * 8, qv);
+      unpack8<T>(qr[r0 + r], qv);
       float mx = -INFINITY;
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
@@ -1082,11 +1094,16 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
   __syncthreads();
   if (!last || !mine) return;
   constexpr int NSMAX = 8;
-  float ms[NSMAX], ls[NSMAX];
+  // every partial in flight before the first use: unconditional loads at a clamped chunk index (a load under
+  // `qq2 < ns` feeding the fma chain waited vmcnt(0) per load), the chunks past ns masked in the arithmetic
+  float ms[NSMAX], ls[NSMAX], op[NSMAX][8];
 #pragma unroll
   for (int qq2 = 0; qq2 < NSMAX; ++qq2) {
-    ms[qq2] = qq2 < ns ? __hip_atomic_load(part + qq2 * (HD + 2), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -INFINITY;
-    ls[qq2] = qq2 < ns ? __hip_atomic_load(part + qq2 * (HD + 2) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+    const float* pq = part + min(qq2, ns - 1) * (HD + 2);
+    ms[qq2] = __hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ls[qq2] = __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) op[qq2][e] = __hip_atomic_load(pq + 2 + td + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   float M = -INFINITY;
 #pragma unroll
@@ -1104,7 +1121,7 @@ __global__ __launch_bounds__(256) void cross_attn_mfma_kernel(const bf16_t* __re
     float ot = 0.f;
 #pragma unroll
     for (int qq2 = 0; qq2 < NSMAX; ++qq2)
-      if (qq2 < ns) ot = fmaf(__hip_atomic_load(part + qq2 * (HD + 2) + 2 + td + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), f[qq2], ot);
+      if (qq2 < ns) ot = fmaf(op[qq2][e], f[qq2], ot);
     orow[e] = f2bf(ot * inv);
   }
 }

@@ -275,10 +275,14 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
   const int per = (V + BSPLIT - 1) / BSPLIT;
   const int v0 = sl * per, v1 = min(V, v0 + per);
   float xv[BUNR];
+  bool mk[BUNR];  // SuppressTokens bytes with the logits (a mask load in the compare chain waits per element)
 #pragma unroll
   for (int u = 0; u < BUNR; ++u) {
-    const int v = v0 + tid + u * BT_S;
-    xv[u] = v < v1 ? x[v] : -INFINITY;
+    const int v = v0 + tid + u * BT_S, vc = min(v, v1 - 1);  // unconditional (clamped) loads: no branches
+    const float xr = x[vc];                                           // and phis between them
+    const uint8_t mr = a.suppress_mask[vc];
+    xv[u] = v < v1 ? xr : -INFINITY;
+    mk[u] = v < v1 ? mr != 0 : true;
   }
   // row state from the history (as kwp::row_state, BT_S threads): the last timestamp position travels with
   // its token in one 64-bit key (no dependent reload), the last two tokens are read up front
@@ -318,7 +322,7 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
   for (int u = 0; u < BUNR; ++u) {
     const int v = v0 + tid + u * BT_S;
     mr = fmaxf(mr, xv[u]);
-    sv[u] = v < v1 ? process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, xv[u]) : -INFINITY;
+    sv[u] = v < v1 ? process_m(st, mk[u], a.begin_suppress, a.n_begin_suppress, v, xv[u]) : -INFINITY;
     if (v < v1) {
       if (v < st.ts_begin) {
         if (better(sv[u], v, mt, it)) { mt = sv[u]; it = v; }

@@ -21,9 +21,12 @@ struct RowState {
   int ban_text;
 };
 
-__device__ __forceinline__ float process(const RowState& st, const uint8_t* __restrict__ mask,
-                                         const int32_t* __restrict__ bsup, int nbsup, int v, float x) {
-  if (mask[v]) return -INFINITY;
+// process() with the SuppressTokens flag of v already loaded: the split kernels fetch the mask bytes of their
+// slice together with the logits (a mask load inside the per-element compare chain cost one vmcnt(0) round
+// trip per element)
+__device__ __forceinline__ float process_m(const RowState& st, bool masked, const int32_t* __restrict__ bsup,
+                                           int nbsup, int v, float x) {
+  if (masked) return -INFINITY;
   if (st.first_step) {
     for (int i = 0; i < nbsup; ++i)
       if (bsup[i] == v) return -INFINITY;
@@ -45,6 +48,11 @@ __device__ __forceinline__ float process(const RowState& st, const uint8_t* __re
     if (st.ban_text && v < st.ts_begin) return -INFINITY;
   }
   return x;
+}
+
+__device__ __forceinline__ float process(const RowState& st, const uint8_t* __restrict__ mask,
+                                         const int32_t* __restrict__ bsup, int nbsup, int v, float x) {
+  return process_m(st, mask[v] != 0, bsup, nbsup, v, x);
 }
 
 __device__ float block_reduce_max(float v, float* sh) {

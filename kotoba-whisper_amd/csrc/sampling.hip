@@ -111,31 +111,40 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_kernel(kw_sampler_a
   const int per = (V + NSPLIT - 1) / NSPLIT;
   const int v0 = sl * per, v1 = min(V, v0 + per);
   const bool first = L == a.begin_index;
+  // the slice's logits and SuppressTokens bytes all in flight first (a mask load inside the compare chain
+  // below cost one round trip per element; the history scan's loop waits on every load it has issued)
+  float xv[SUNR];
+  bool mk[SUNR];
+#pragma unroll
+  for (int u = 0; u < SUNR; ++u) {
+    const int v = v0 + tid + u * SPLIT_T, vc = min(v, v1 - 1);  // unconditional (clamped) loads: no branches
+    const float xr = x[vc];                                           // and phis between them
+    const uint8_t mr = a.suppress_mask[vc];
+    xv[u] = v < v1 ? xr : -INFINITY;
+    mk[u] = v < v1 ? mr != 0 : true;
+  }
   // a row is finished once it emitted EOS (stopping_criteria.py:75-77): one id per thread, in parallel
   // (the row's last arriver needs it; a serial walk there would pay one load latency per position)
   int fin = 0;
   for (int p = a.begin_index + tid; p < L; p += SPLIT_T) fin |= ids[p] == a.eos_id;
-  float xv[SUNR];
-#pragma unroll
-  for (int u = 0; u < SUNR; ++u) {
-    const int v = v0 + tid + u * SPLIT_T;
-    xv[u] = v < v1 ? x[v] : -INFINITY;
-  }
   float best = -INFINITY;
   int bi = 0x7fffffff;
   for (int vb = v0; vb < v1; vb += SPLIT_T * SUNR) {  // one round for V <= NSPLIT * 8192
     if (vb != v0) {
 #pragma unroll
       for (int u = 0; u < SUNR; ++u) {
-        const int v = vb + tid + u * SPLIT_T;
-        xv[u] = v < v1 ? x[v] : -INFINITY;
+        const int v = vb + tid + u * SPLIT_T, vc = min(v, v1 - 1);  // unconditional (clamped) loads: no branches
+        const float xr = x[vc];                                           // and phis between them
+        const uint8_t mr = a.suppress_mask[vc];
+        xv[u] = v < v1 ? xr : -INFINITY;
+        mk[u] = v < v1 ? mr != 0 : true;
       }
     }
 #pragma unroll
     for (int u = 0; u < SUNR; ++u) {
       const int v = vb + tid + u * SPLIT_T;
       if (v < v1) {
-        float s = a.suppress_mask[v] ? -INFINITY : xv[u];
+        float s = mk[u] ? -INFINITY : xv[u];
         if (first)
           for (int i = 0; i < a.n_begin_suppress; ++i)
             if (a.begin_suppress[i] == v) s = -INFINITY;
@@ -246,10 +255,14 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_ts_kernel(kw_sample
   const int per = (V + NSPLIT - 1) / NSPLIT;
   const int v0 = sl * per, v1 = min(V, v0 + per);
   float xv[SUNR];
+  bool mk[SUNR];
 #pragma unroll
-  for (int u = 0; u < SUNR; ++u) {  // the slice's logits in flight while the history is scanned
-    const int v = v0 + tid + u * SPLIT_T;
-    xv[u] = v < v1 ? x[v] : -INFINITY;
+  for (int u = 0; u < SUNR; ++u) {  // the slice's logits and mask bytes in flight while the history is scanned
+    const int v = v0 + tid + u * SPLIT_T, vc = min(v, v1 - 1);  // unconditional (clamped) loads: no branches
+    const float xr = x[vc];                                           // and phis between them
+    const uint8_t mr = a.suppress_mask[vc];
+    xv[u] = v < v1 ? xr : -INFINITY;
+    mk[u] = v < v1 ? mr != 0 : true;
   }
   // ---- row state from the id history (as kwp::row_state, 512 threads) ----
   int fin = 0, lsp = -1;
@@ -286,7 +299,7 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_ts_kernel(kw_sample
 #pragma unroll
   for (int u = 0; u < SUNR; ++u) {
     const int v = v0 + tid + u * SPLIT_T;
-    sv[u] = v < v1 ? process(st, a.suppress_mask, a.begin_suppress, a.n_begin_suppress, v, xv[u]) : -INFINITY;
+    sv[u] = v < v1 ? process_m(st, mk[u], a.begin_suppress, a.n_begin_suppress, v, xv[u]) : -INFINITY;
     if (v < v1) {
       if (v < st.ts_begin) {
         if (sv[u] > mt || (sv[u] == mt && v < it)) { mt = sv[u]; it = v; }
