@@ -690,7 +690,9 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   const int g0 = blockIdx.x * groups_per_wg, g1 = min(n_groups, g0 + groups_per_wg);
   if (g0 >= g1) return;
   const int n_cb = (p.N + 15) / 16;
-  auto wload = [&](int g, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
+  // a group's weights AND the column sum / bias its epilogue waves (0..2*NCB-1) need, in one batch: an
+  // epilogue load issued after the next group's prefetch waits for that prefetch too (vmcnt is in order)
+  auto wload = [&](int g, bf16x8 (&w)[LMH_NCB][LMH_KTM], float& ecs, float& ebn) {
 #pragma unroll
     for (int c = 0; c < LMH_NCB; ++c) {
       const int cb = min(g * LMH_NCB + c, n_cb - 1);
@@ -698,9 +700,13 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       for (int u = 0; u < LMH_KTM; ++u)
         w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)cb * nkt + min(kt0 + u, ktl)) * 64 + lane);
     }
+    const int n = min((g * LMH_NCB + ((wave >> 1) & (LMH_NCB - 1))) * 16 + (lane & 15), p.N - 1);
+    ecs = p.ln_colsum[n];
+    ebn = p.bias ? p.bias[n] : 0.f;
   };
   bf16x8 wa[LMH_NCB][LMH_KTM], wb[LMH_NCB][LMH_KTM];
-  wload(g0, wa);
+  float csa, bna, csb, bnb;
+  wload(g0, wa, csa, bna);
   // activation fragments of this wave's k-range, once (rows lane&15 and 16 + lane&15)
   bf16x8 a0[LMH_KTM], a1[LMH_KTM];
   {
@@ -752,7 +758,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
     }
   }
   // walk the run: weights of group g+1 in flight while group g is multiplied, reduced and stored
-  auto body = [&](int g, int par, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
+  auto body = [&](int g, int par, bf16x8 (&w)[LMH_NCB][LMH_KTM], float cs, float bn) {
     f32x4 c0[LMH_NCB], c1[LMH_NCB];
 #pragma unroll
     for (int c = 0; c < LMH_NCB; ++c) {
@@ -775,7 +781,6 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       for (int w2 = 1; w2 < nw; ++w2) acc += red[par][w2][c][hh][lane];
       const int n = (g * LMH_NCB + c) * 16 + (lane & 15);
       if (n < p.N) {
-        const float cs = p.ln_colsum[n], bn = p.bias ? p.bias[n] : 0.f;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = 16 * hh + 4 * (lane >> 4) + r;
@@ -789,12 +794,12 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   };
   int par = 0;
   for (int g = g0; g < g1; g += 2) {
-    if (g + 1 < g1) wload(g + 1, wb);
-    body(g, par, wa);
+    if (g + 1 < g1) wload(g + 1, wb, csb, bnb);
+    body(g, par, wa, csa, bna);
     par ^= 1;
     if (g + 1 >= g1) break;
-    if (g + 2 < g1) wload(g + 2, wa);
-    body(g + 1, par, wb);
+    if (g + 2 < g1) wload(g + 2, wa, csa, bna);
+    body(g + 1, par, wb, csb, bnb);
     par ^= 1;
   }
 }
