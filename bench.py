@@ -10,7 +10,8 @@ time is the max over ranks.
 
 Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` of the decode attention (the cross-attention's
 stream of the encoder output, HBM-bound), ``encoder_mfma`` (encoder MFMA fraction), ``decode_kernel_us``
-(per-launch device time of each decode-step kernel, in step context), ``cpu_baseline`` (reference
+(per-launch time of each decode-step kernel in step context, eager: an upper bound that includes the
+dispatch gap; the rocprofv3 trace in profiles/ gives the device times), ``cpu_baseline`` (reference
 transformers path on the host cores, bounded sample).
 """
 from __future__ import annotations
@@ -279,6 +280,9 @@ def main():
                          "frac": ENC_FLOP_PER_CLIP * B / enc_t / 1e12 / BF16_PEAK_TFLOPS},
         "decode_step_ms": step_t * 1e3 if step_t else None,
         "decode_kernel_us": kern_us,
+        "decode_kernel_us_note": ("eager launches in step order with HIP events around each: includes the host "
+                                  "dispatch gap a graph replay does not have; device times per kernel are the "
+                                  "rocprofv3 trace averages under profiles/"),
     }
     traffic, src = pmc_traffic(cross_kernel)
     result["roofline"]["traffic"] = traffic
