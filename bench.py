@@ -2,14 +2,15 @@
 """Headline benchmark: audio-seconds/sec of whisper-large-v3 greedy generate, 30 s clips, batch 32/GPU.
 
 One step = one batch of 32 synthetic 30 s clips resident in HBM -> log-mel (HIP) -> encoder ->
-greedy decode (cross-attention read from the encoder output: kw_cross_attn_enc) (4-token prompt, max_length 128 -> 128 new tokens, hipGraph step) on the
+cross-attention K/V projection -> greedy decode (4-token prompt, max_length 128 -> 128 new tokens, one hipGraph
+replay per step; cross-attention over the per-layer K/V cache, cross_attn_dma_kernel) on the
 MI355X engine (bf16).  Weights are random-init of the large-v3 architecture (no checkpoints offline).
 N > 1: one process per GPU (torchrun), each rank decodes its own batches (data parallel, weak
 scaling), token ids are all-gathered over RCCL at the end (run_pseudo_labelling.py:339-341), and the
 time is the max over ranks.
 
 Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` of the decode attention (the cross-attention's
-stream of the encoder output, HBM-bound), ``encoder_mfma`` (encoder MFMA fraction), ``decode_kernel_us``
+K/V stream, HBM-bound; the kw_cross_attn_enc kernel when the engine runs cross_attention="encoder_output"), ``encoder_mfma`` (encoder MFMA fraction), ``decode_kernel_us``
 (per-launch time of each decode-step kernel in step context, eager: an upper bound that includes the
 dispatch gap; the rocprofv3 trace in profiles/ gives the device times), ``cpu_baseline`` (reference
 transformers path on the host cores, bounded sample).
