@@ -9,8 +9,12 @@ N > 1: one process per GPU (torchrun), each rank decodes its own batches (data p
 scaling), token ids are all-gathered over RCCL at the end (run_pseudo_labelling.py:339-341), and the
 time is the max over ranks.
 
+``--gpus N`` without a launcher's WORLD_SIZE starts ``python -m torch.distributed.run --nproc-per-node N`` on
+this script as a CHILD process (nothing touches the GPU in the parent) and relays rank 0's line, as the
+reference's ``accelerate launch --multi_gpu`` (script/distil_whisper_v2.0.sh:26) starts one process per GPU.
+
 Prints ONE JSON line (rank 0).  Extra fields: ``roofline`` of the decode attention (the cross-attention's
-K/V stream, HBM-bound; the kw_cross_attn_enc kernel when the engine runs cross_attention="encoder_output"), ``encoder_mfma`` (encoder MFMA fraction), ``decode_kernel_us``
+K/V stream, HBM-bound), ``encoder_mfma`` (encoder MFMA fraction), ``decode_kernel_us``
 (per-launch time of each decode-step kernel in step context, eager: an upper bound that includes the
 dispatch gap; the rocprofv3 trace in profiles/ gives the device times), ``cpu_baseline`` (reference
 transformers path on the host cores, bounded sample).
@@ -36,17 +40,27 @@ BF16_PEAK_TFLOPS = 2500.0      # dense bf16 MFMA spec
 ENC_FLOP_PER_CLIP = 2.2738e12
 
 
+def kernel_source_files() -> list:
+    """The product kernel sources: the ``SRCS`` of csrc/Makefile (what libkwhisper.so is built from), the
+    csrc headers they include and include/kwhisper.h.  Read from the Makefile, not globbed, so scratch
+    files beside them never change the hash, and no git is needed (the GPU box's snapshot has none)."""
+    import re
+
+    csrc = os.path.join(ROOT, "kotoba-whisper_amd", "csrc")
+    with open(os.path.join(csrc, "Makefile")) as f:
+        m = re.search(r"^SRCS\s*:=\s*(.+)$", f.read(), re.M)
+    srcs = m.group(1).split()
+    heads = ("kw_common.h", "gemm_common.h", "processors.h")
+    return [os.path.join(csrc, x) for x in srcs + list(heads)] + [os.path.join(ROOT, "include", "kwhisper.h")]
+
+
 def kernel_source_hash() -> str:
-    """sha256 over the kernel sources (csrc/*.hip, *.h, include/kwhisper.h): identifies the kernels a PMC pass
-    measured (tools/profile.sh stores it beside the counters)."""
-    import glob
+    """sha256 over kernel_source_files(): identifies the kernels a PMC pass measured (tools/profile.sh
+    stores it beside the counters, on the GPU box; that box-side file is committed as it was written)."""
     import hashlib
 
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(ROOT, "kotoba-whisper_amd", "csrc", "*.hip")) +
-                   glob.glob(os.path.join(ROOT, "kotoba-whisper_amd", "csrc", "*.h")) +
-                   [os.path.join(ROOT, "include", "kwhisper.h")])
-    for f in files:
+    for f in kernel_source_files():
         h.update(os.path.basename(f).encode())
         with open(f, "rb") as fh:
             h.update(fh.read())
@@ -88,7 +102,7 @@ def pmc_traffic(kernel: str):
     return None, f"{rel} has no {kernel} row"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
@@ -97,24 +111,98 @@ def parse():
     ap.add_argument("--max-length", type=int, default=128)
     ap.add_argument("--model", default="large-v3")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--kernel-iters", type=int, default=20)
-    ap.add_argument("--pipeline", action="store_true",
-                    help="generate_pipelined: the next batch's log-mel/encoder/cross-K/V on CUs [0, --encoder-cus) "
-                         "beside this batch's decode (measured slower on 1x MI355X: profiles/r01e_lab_notes.md)")
-    ap.add_argument("--encoder-cus", type=int, default=64)
-    return ap.parse_args()
+    ap.add_argument("--stub", action="store_true",
+                    help="no GPU work: each rank times a trivial host step (tests the launcher, barriers, "
+                         "max-over-ranks timing and the ids gather on the CPU; with KW_BENCH_BACKEND=gloo)")
+    return ap.parse_args(argv)
 
 
-def main():
-    a = parse()
+def launch_ranks(a, argv) -> int:
+    """``--gpus N`` (N > 1) without WORLD_SIZE: one process per GPU under torch.distributed.run, started as a
+    child (never exec: this process has not touched the GPU and stays the parent), rank 0's JSON line
+    relayed.  Returns the launcher's exit code."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "16")
+    proc = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    line = None
+    for ln in proc.stdout.splitlines():
+        if ln.startswith("{") and '"metric"' in ln:
+            line = ln
+        else:
+            print(ln, flush=True)
+    if line is not None:
+        print(line, flush=True)
+    return proc.returncode if line is not None or proc.returncode else 1
+
+
+def stub_main(a, world, rank, dist):
+    """The multi-rank bench skeleton without a GPU: a fixed host step per rank, the same barrier +
+    max-over-ranks timing and the same (padded) ids gather as main()."""
+    import torch
+
+    def step():
+        x = torch.ones(256, 256)
+        for _ in range(4):
+            x = x @ x / 256.0
+        return torch.full((a.batch, 8), rank, dtype=torch.int32)
+
+    for _ in range(a.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    ids = [step() for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        gathered = [torch.empty_like(ids[-1]) for _ in range(world)]
+        dist.all_gather(gathered, ids[-1])
+        assert [int(g[0, 0]) for g in gathered] == list(range(world))
+    dt = float(t.item())
+    out = {"metric": "audio-seconds/sec (RTF) whisper-large-v3 30s@bs32", "value": world * a.batch * 30.0 * a.steps / dt,
+           "unit": "audio-s/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
+           "ms_per_step": dt / a.steps * 1e3, "stub": True,
+           "dist": {"world": world, "backend": dist.get_backend() if world > 1 else None}}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a, argv))  # before anything touches the GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    backend = os.environ.get("KW_BENCH_BACKEND", "nccl")
+    if a.stub:
+        if world > 1:
+            dist.init_process_group(backend)
+        stub_main(a, world, rank, dist)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     # one process per GPU; more ranks than GPUs only in a rehearsal (KW_BENCH_BACKEND=gloo on a 1-GPU box)
-    local = local % max(1, torch.cuda.device_count())
+    ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise RuntimeError("bench.py needs a HIP device (use --stub to exercise the launcher on the CPU)")
+    local = local % ndev
     if world > 1:
-        backend = os.environ.get("KW_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -140,19 +228,9 @@ def main():
     gen_kw = dict(language="ja", task="transcribe", max_length=a.max_length, return_timestamps=False)
     out_ids = []
 
-    if not a.pipeline:
-        def batches(n):
-            for _ in range(n):
-                yield model.generate(fe.extract(audio), **gen_kw)
-    else:
-        # one generator over warmup + timed batches: the first timed batch's encoder already ran beside the
-        # last warmup decode, as every later batch's runs beside its predecessor's (steady state)
-        stream_of = model.generate_pipelined((audio for _ in range(a.warmup + a.steps)), feature_extractor=fe,
-                                             encoder_cus=a.encoder_cus, **gen_kw)
-
-        def batches(n):
-            for _ in range(n):
-                yield next(stream_of)
+    def batches(n):
+        for _ in range(n):
+            yield model.generate(fe.extract(audio), **gen_kw)
 
     for ids in batches(a.warmup):
         out_ids.append(ids)
@@ -227,28 +305,19 @@ def main():
         return {k: round(tot[k] / cnt[k], 2) for k in tot}
 
     kern_us = step_kernel_times()
-    if sess.use_enc:
-        # cross-attention over the encoder output: algorithmic bytes = the batch's encoder output, read once
-        # per launch (+ the queries u and the output z); one launch per decoder layer, all on the same e
-        cross_kernel = "xattn_enc_kernel"
-        cross_bytes = B * S * shape.d_model * 2 + 2 * B * H * shape.d_model * 2
-        cross_t = kern_us["xenc"] * 1e-6
-        cross_note = ("xattn_enc_kernel (decoder cross-attention over the encoder output, K/V projections absorbed; "
-                      "one launch per layer; rocprof name)")
-    else:
-        qx = sess._buffers(1)["qx"]
-        attn_out = sess._buffers(1)["attn"]
-        ws = sess._buffers(1)["ws"]
+    qx = sess._buffers(1)["qx"]
+    attn_out = sess._buffers(1)["attn"]
+    ws = sess._buffers(1)["ws"]
 
-        def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
-            for li in range(n_dec):
-                ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[2 * li], sess.cross[2 * li + 1], S, attn_out, ws)
+    def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
+        for li in range(n_dec):
+            ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[2 * li], sess.cross[2 * li + 1], S, attn_out, ws)
 
-        cross_kernel = "cross_attn_dma_kernel"
-        cross_t = time_fn(cross_all_layers, max(1, iters // 4)) / n_dec
-        cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
-        cross_note = ("cross_attn_dma_kernel (decoder cross-attention K/V stream, K by LDS-DMA, one launch per layer; "
-                      "rocprof name)")
+    cross_kernel = "cross_attn_dma_kernel"
+    cross_t = time_fn(cross_all_layers, max(1, iters // 4)) / n_dec
+    cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
+    cross_note = ("cross_attn_dma_kernel (decoder cross-attention K/V stream, K by LDS-DMA, one launch per layer; "
+                  "rocprof name)")
     feats = fe.extract(audio)
     enc_t = time_fn(lambda: eng.encode(feats), 3)
     step_graph = sess._graph
@@ -271,8 +340,10 @@ def main():
         "config": {"workload": "config 3: whisper-large-v3 greedy generate, 30 s clips, log-mel on GPU",
                    "model": shape.name, "global_batch": B * world, "per_gpu_batch": B,
                    "max_length": a.max_length, "new_tokens": new_tokens, "seq_len": 1500,
-                   "pipelined": a.pipeline, "encoder_cus": a.encoder_cus if a.pipeline else None,
                    "parallelism": f"dp{world}"},
+        "dist": {"world": world, "rank_device": local, "device_name": torch.cuda.get_device_name(dev),
+                 "backend": dist.get_backend() if world > 1 else None,
+                 "ids_gather": "all_gather of the padded int32 token matrices" if world > 1 else None},
         "roofline": {"kernel": cross_note,
                      "bound": "hbm", "achieved": cross_bytes / cross_t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": cross_bytes / cross_t / 1e9 / HBM_PEAK_GBS, "traffic": None,
@@ -291,14 +362,15 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle.cpu_baseline import hf_cpu_generate_rate
 
-        cb = hf_cpu_generate_rate(shape, a.cpu_batch, a.max_length)
+        cb = hf_cpu_generate_rate(shape, a.cpu_batch, a.max_length, threads=a.cpu_threads)
         result["cpu_baseline"] = {
             "value": cb["audio_seconds_per_second"], "unit": "audio-s/s", "cores": cb["threads"], "kind": "reference",
             "threads": cb["threads"], "nproc": cb["nproc"], "affinity_cpus": cb["affinity_cpus"],
             "sample": f"transformers 5.15.0 WhisperForConditionalGeneration.generate fp32 on CPU, torch "
-                      f"{cb['threads']} intra-op threads (the box shows nproc {cb['nproc']}, {cb['affinity_cpus']} in "
-                      f"this process's affinity), a bounded sample of {a.cpu_batch} clips x 30 s (not the config's 32: "
-                      f"about {cb['seconds'] * 32 / max(1, a.cpu_batch) / 60:.0f} min of CPU at 32 if the rate held), "
+                      f"{cb['threads']} intra-op threads = this process's CPU affinity ({cb['affinity_cpus']}) capped by "
+                      f"OMP_NUM_THREADS ({os.environ.get('OMP_NUM_THREADS')}, the host-CPU share of one GPU; the node "
+                      f"shows nproc {cb['nproc']}), a bounded sample of {a.cpu_batch} clips x 30 s (the config's 32-clip "
+                      f"batch at the same thread count: profiles/r03_cpu_baseline_b32.json), "
                       f"greedy, {cb['new_tokens']} new tokens, {cb['seconds']:.1f} s; run_speed_eval.py:73-78 timing"}
     if rank == 0:
         print(json.dumps(result), flush=True)

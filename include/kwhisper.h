@@ -29,13 +29,8 @@ enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
 enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 
 /* ABI version (major*100 + minor) and the last error message of this thread. */
-int kw_version(void);  /* 103 */
+int kw_version(void);  /* 104 */
 const char* kw_last_error(void);
-
-/* A stream whose kernels run only on CUs [cu_begin, cu_end) (hipExtStreamCreateWithCUMask), and its
- * release.  Used to run the next batch's encoder beside the current batch's decode steps. */
-int kw_stream_create_cu_range(int cu_begin, int cu_end, kw_stream_t* out);
-int kw_stream_destroy(kw_stream_t stream);
 
 /* a1 -- log-mel spectrogram.
  * Replaces WhisperFeatureExtractor._torch_extract_fbank_features (TF/models/whisper/
@@ -93,10 +88,6 @@ int kw_gemm(const kw_gemm_args* args, kw_stream_t stream);
  *   STORE: C[m][n] = act(acc + bias) * (n < scale_cols ? scale : 1), C f32 or bf16;
  *   RESID: h[m][n] += acc + bias (f32 residual, modeling_whisper.py:482,495,503) and hb = bf16(h), the
  *          bf16 mirror the next LayerNorm-fused linear reads.
- * Grouped activations (x_group_cols > 0, a multiple of 32, no ln): output column n reads the activation row
- *   at x + (n / x_group_cols) * x_group_stride -- the per-head projections of kw_cross_attn_enc's query side
- *   (u_h = Wk_h^T q_h: K = head_dim, groups of D columns, stride head_dim) and value side (Wv_h z_h: K = D,
- *   groups of head_dim columns, stride D).
  * W: packed by kw_pack_weight.  workspace: >= kw_dec_linear_workspace_bytes(N, K) bytes, zero-filled
  * before first use (calls leave it zeroed); one workspace may serve all calls on one stream.
  * Results are bitwise deterministic (fixed-order reductions, no float atomics). */
@@ -121,8 +112,6 @@ typedef struct {
   int64_t M, N, K;
   void* workspace;
   size_t ws_bytes;
-  int64_t x_group_cols;      /* 0: every column reads x's row (no groups) */
-  int64_t x_group_stride;    /* elements between consecutive groups' activations */
 } kw_dec_linear_args;
 
 int kw_dec_linear(const kw_dec_linear_args* args, kw_stream_t stream);
@@ -175,19 +164,6 @@ int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64
                        const void* k, const void* v, int64_t S, void* out, void* workspace,
                        size_t ws_bytes, kw_stream_t stream);
 size_t kw_cross_attn_workspace(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S);
-
-/* Decoder cross-attention read from the encoder output itself, the cross K/V projections absorbed into
- * the query and value sides (replaces TF modeling_whisper.py:323-335's cache + sdpa_attention.py:79-166 for
- * the cross-attention; the K/V cache of cache_utils.py:1940-2038 is never built).  With
- * k_f = Wk_h e_f and v_f = Wv_h e_f + bv_h:  q_h . k_f = u_h . e_f  (u_h = Wk_h^T q_h) and
- * softmax(q_h K^T) V = Wv_h z_h + bv_h with z_h = sum_f softmax_f(u_h . e_f) e_f.  This call computes z:
- *   enc: [B][S][D] bf16 (the encoder's last_hidden_state); u: [B*q_len][H][D] bf16 (row b*q_len + i, head h);
- *   z:   [B*q_len][H][D] bf16.  D in {384, 512, 768, 1024, 1280}, H <= 32, pointers 16-B aligned.
- * workspace >= kw_cross_attn_enc_workspace(B, D) bytes, ZERO-FILLED before first use (arrival counters that
- * every call leaves at zero).  Deterministic (fixed-order reductions). */
-int kw_cross_attn_enc(const void* enc, int64_t B, int64_t S, int64_t D, const void* u, int64_t q_len, int64_t H,
-                      void* z, void* workspace, size_t ws_bytes, kw_stream_t stream);
-size_t kw_cross_attn_enc_workspace(int64_t B, int64_t D);
 
 /* One greedy decoding step on f32 logits [B][V] (TF generation/utils.py:2894-2937):
  * SuppressTokens -> SuppressTokensAtBegin (when L == begin_index) -> WhisperTimeStamp (if

@@ -69,8 +69,6 @@ struct DecP {
   float* slab;
   int* cnt;
   int xlds;  // stage the activation rows through LDS (single-round, no-split-K grids)
-  int gw;    // grouped activations: output columns [g*gw, (g+1)*gw) read x + g*gx (gw = 0: one group)
-  int64_t gx;
 };
 
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
@@ -92,7 +90,6 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
   } else {
     p.M = min(32, p0.M);
   }
-  if (p.gw) p.x += (int64_t)((blockIdx.x * NCB * 16) / p.gw) * p.gx;  // the workgroup's activation group
   __shared__ f32x4 red[MAXW][NCB][2][64];
   __shared__ float rpart[MAXW][32][2];  // LayerNorm: per-wave row (sum, sum of squares)
   __shared__ float rstat[32][2];     // LayerNorm: (mean, rstd) per row
@@ -354,7 +351,6 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
 // so results are bitwise those of the chunked launch.
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
 __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) {
-  if (p.gw) p.x += (int64_t)((blockIdx.x * NCB * 16) / p.gw) * p.gx;  // the workgroup's activation group
   __shared__ f32x4 red[MAXW][NCB][2][64];
   __shared__ float rpart[MAXW][32][2];
   __shared__ float rstat[32][2];
@@ -950,11 +946,6 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
   }
   if (a->ln && (!a->ln_colsum || a->epilogue != KW_EPI_STORE))
     return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: fused LayerNorm needs ln_colsum and the STORE epilogue");
-  if (a->x_group_cols < 0 || a->x_group_stride < 0 || (a->x_group_cols && (a->x_group_cols % 32 || a->ln)) ||
-      (a->x_group_stride % 8) != 0)
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: x groups need x_group_cols % 32 == 0, x_group_stride % 8 == 0, no ln");
-  if (a->x_group_cols && ((a->N + a->x_group_cols - 1) / a->x_group_cols - 1) * a->x_group_stride + a->K > a->ldx)
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_linear: the last x group's K columns run past ldx");
   if (a->M == 0) return KW_OK;
   const Geo g = choose(a->N, a->K);
   const int nkt = (int)(a->K / 32);
@@ -1024,8 +1015,6 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     p.cnt = reinterpret_cast<int*>(a->workspace);
     p.slab = a->workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(a->workspace) + CNT_MAX * sizeof(int)) : nullptr;
     p.xlds = use_xlds(a->N, g) ? 1 : 0;
-    p.gw = (int)a->x_group_cols;
-    p.gx = a->x_group_stride;
     if (lmh) {
       static int ncu = 0;
       if (!ncu) {

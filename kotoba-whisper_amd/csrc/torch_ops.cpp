@@ -115,13 +115,13 @@ void gemm(const Tensor& A, const Tensor& W, const optional<Tensor>& bias, Tensor
 }
 
 // ---- decode-step linear over packed weights -----------------------------------------------------------
-// geo = [x_offset, ldx, ln, c_offset, ldc, gelu, scale_cols, resid_row0, ldh, M, N, K, x_group_cols, x_group_stride]
+// geo = [x_offset, ldx, ln, c_offset, ldc, gelu, scale_cols, resid_row0, ldh, M, N, K]
 void dec_linear(const Tensor& x, const Tensor& W, const optional<Tensor>& bias, const optional<Tensor>& ln_colsum,
                 optional<Tensor> C, optional<Tensor> h, optional<Tensor> hb, Tensor& workspace,
                 std::vector<int64_t> geo, double ln_eps, double scale) {
   const char* w = "kw_dec_linear";
   dev(x, w), dev(W, w), dev(bias, w), dev(ln_colsum, w), dev(C, w), dev(h, w), dev(hb, w), dev(workspace, w);
-  TORCH_CHECK_VALUE(geo.size() == 14, "kw_dec_linear: geo must hold 14 integers");
+  TORCH_CHECK_VALUE(geo.size() == 12, "kw_dec_linear: geo must hold 12 integers");
   TORCH_CHECK_VALUE(x.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16,
                     "kw_dec_linear takes bf16 activations and packed bf16 weights");
   kw_dec_linear_args a{};
@@ -150,7 +150,6 @@ void dec_linear(const Tensor& x, const Tensor& W, const optional<Tensor>& bias, 
   a.scale = (float)scale;
   a.scale_cols = geo[6];
   a.M = geo[9], a.N = geo[10], a.K = geo[11];
-  a.x_group_cols = geo[12], a.x_group_stride = geo[13];
   a.workspace = ptr(workspace);
   a.ws_bytes = (size_t)workspace.numel() * workspace.element_size();
   c10::DeviceGuard g(W.device());
@@ -224,19 +223,6 @@ void cross_attn_step(const Tensor& q, int64_t B, int64_t q_len, int64_t H, int64
   c10::DeviceGuard g(q.device());
   check(kw_cross_attn_step(dt_of(q), ptr(q), B, q_len, H, hd, ptr(k), ptr(v), S, ptr(out), ptr(workspace),
                            (size_t)workspace.numel() * workspace.element_size(), stream_of(q)),
-        w);
-}
-
-void cross_attn_enc(const Tensor& enc, int64_t B, int64_t S, int64_t D, const Tensor& u, int64_t q_len, int64_t H,
-                    Tensor& z, Tensor& workspace) {
-  const char* w = "kw_cross_attn_enc";
-  dev(enc, w), dev(u, w), dev(z, w), dev(workspace, w);
-  TORCH_CHECK_VALUE(enc.scalar_type() == at::kBFloat16 && u.scalar_type() == at::kBFloat16 &&
-                        z.scalar_type() == at::kBFloat16,
-                    "kw_cross_attn_enc takes bf16 enc / u / z");
-  c10::DeviceGuard g(u.device());
-  check(kw_cross_attn_enc(ptr(enc), B, S, D, ptr(u), q_len, H, ptr(z), ptr(workspace),
-                          (size_t)workspace.numel() * workspace.element_size(), stream_of(u)),
         w);
 }
 
@@ -349,7 +335,6 @@ int64_t workspace_bytes(std::string kind, std::vector<int64_t> d) {
   if (kind == "packed_weight") return (int64_t)kw_packed_weight_bytes(n(0), n(1));
   if (kind == "self_attn") return (int64_t)kw_self_attn_workspace(n(0), n(1), n(2));
   if (kind == "cross_attn") return (int64_t)kw_cross_attn_workspace(n(0), n(1), n(2), n(3), n(4));
-  if (kind == "cross_attn_enc") return (int64_t)kw_cross_attn_enc_workspace(n(0), n(1));
   if (kind == "greedy_step") return (int64_t)kw_greedy_step_workspace(n(0));
   if (kind == "beam_logprobs") return (int64_t)kw_beam_logprobs_workspace(n(0));
   TORCH_CHECK_VALUE(false, "kw::workspace_bytes: unknown kind ", kind);
@@ -376,8 +361,6 @@ TORCH_LIBRARY(kw, m) {
         "int t_max, Tensor cur_len, Tensor(c!) out, Tensor(d!)? workspace, Tensor? bp) -> ()");
   m.def("cross_attn_step(Tensor q, int B, int q_len, int H, int hd, Tensor k, Tensor v, int S, Tensor(a!) out, "
         "Tensor(b!) workspace) -> ()");
-  m.def("cross_attn_enc(Tensor enc, int B, int S, int D, Tensor u, int q_len, int H, Tensor(a!) z, "
-        "Tensor(b!) workspace) -> ()");
   m.def("greedy_step(Tensor(a!) logits, Tensor suppress_mask, Tensor? begin_suppress, Tensor(b!) ids, "
         "Tensor(c!) cur_len, Tensor(d!) unfinished, Tensor(e!) counter, Tensor(f!) n_unfinished, "
         "Tensor(g!)? scores_out, Tensor(h!)? workspace, int[] cfg) -> ()");
@@ -400,7 +383,6 @@ TORCH_LIBRARY_IMPL(kw, CUDA, m) {
   m.impl("embed", &embed);
   m.impl("self_attn_step", &self_attn_step);
   m.impl("cross_attn_step", &cross_attn_step);
-  m.impl("cross_attn_enc", &cross_attn_enc);
   m.impl("greedy_step", &greedy_step);
   m.impl("beam_logprobs", &beam_logprobs);
   m.impl("beam_select", &beam_select);

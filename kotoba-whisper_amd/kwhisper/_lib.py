@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("KWHISPER_LIB") or os.path.join(os.path.dirname(os.pat
 TORCH_LIB_PATH = os.environ.get("KWHISPER_TORCH_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                       "libkwhisper_torch.so")
 TORCH_OPS = ("log_mel", "mel_to_time_major", "gemm", "dec_linear", "pack_weight", "layernorm", "attention", "embed",
-             "self_attn_step", "cross_attn_step", "cross_attn_enc", "greedy_step", "beam_logprobs", "beam_select")
+             "self_attn_step", "cross_attn_step", "greedy_step", "beam_logprobs", "beam_select")
 
 KW_OK, KW_EINVAL, KW_EHIP, KW_EUNSUPPORTED = 0, 1, 2, 3
 KW_DT_F32, KW_DT_BF16 = 0, 1
@@ -52,7 +52,6 @@ class DecLinearArgs(ctypes.Structure):
         ("h", c_vp), ("hb", c_vp), ("ldh", c_i64),
         ("M", c_i64), ("N", c_i64), ("K", c_i64),
         ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
-        ("x_group_cols", c_i64), ("x_group_stride", c_i64),
     ]
 
 
@@ -94,8 +93,6 @@ class BeamSelectArgs(ctypes.Structure):
 
 EXPORTS = {
     "kw_version": (ctypes.c_int, []),
-    "kw_stream_create_cu_range": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(c_vp)]),
-    "kw_stream_destroy": (ctypes.c_int, [c_vp]),
     "kw_last_error": (ctypes.c_char_p, []),
     "kw_log_mel": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp, c_vp, c_vp]),
     "kw_mel_to_time_major": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp]),
@@ -115,9 +112,6 @@ EXPORTS = {
     "kw_cross_attn_step": (ctypes.c_int, [ctypes.c_int, c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, c_vp, c_i64, c_vp,
                                           c_vp, ctypes.c_size_t, c_vp]),
     "kw_cross_attn_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64, c_i64]),
-    "kw_cross_attn_enc": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, c_i64, c_i64, c_vp, c_vp, ctypes.c_size_t,
-                                         c_vp]),
-    "kw_cross_attn_enc_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
     "kw_greedy_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), c_vp]),
     "kw_greedy_step_workspace": (ctypes.c_size_t, [c_i64]),
     "kw_beam_logprobs": (ctypes.c_int, [ctypes.POINTER(BeamLogprobsArgs), c_vp]),

@@ -1,10 +1,8 @@
 """Device-resident greedy decoding for one batch (WhisperDecoder + GenerationMixin._sample).
 
 A ``DecodeSession`` owns the static caches and step buffers of one batch:
-  * the cross-attention's source: on the bf16 engine with one row per item, the encoder output itself
-    ([B][1500][d], read by kw_cross_attn_enc with the K/V projections absorbed into the query and value
-    linears: no cross K/V cache); otherwise cross K/V of every layer ([2L][B][H][1500][64], one GEMM,
-    TF modeling_whisper.py:323-335);
+  * cross K/V of every layer ([2L][B][H][1500][64], one GEMM, TF modeling_whisper.py:323-335), per item
+    (beams share it);
   * self K/V static cache [L][B][H][448][64] (replaces DynamicLayer's torch.cat growth,
     TF/cache_utils.py:127-145);
   * ids [B][448] int64, cur_len, unfinished flags -- all on device, advanced by kw_greedy_step.
@@ -34,14 +32,7 @@ class DecodeSession:
         dev, dt = eng.device, eng.dtype
         d, H, Ld = s.d_model, eng.H, s.decoder_layers
         self.T = s.max_source_positions
-        self.use_enc = eng.xattn_enc and beams == 1
-        if self.use_enc:
-            self.cross = None
-            self.enc = torch.empty((B * self.T, d), device=dev, dtype=dt)  # session copy of the encoder output
-            self.xenc_ws = torch.zeros(((ops.cross_attn_enc_workspace_bytes(B, d) + 3) // 4,), device=dev,
-                                       dtype=torch.float32)
-        else:
-            self.cross = torch.empty((2 * Ld, B, H, self.T, _HD), device=dev, dtype=dt)
+        self.cross = torch.empty((2 * Ld, B, H, self.T, _HD), device=dev, dtype=dt)
         self.kc = torch.zeros((Ld, R, H, T_MAX, _HD), device=dev, dtype=dt)
         self.vc = torch.zeros((Ld, R, H, T_MAX, _HD), device=dev, dtype=dt)
         self.ids = torch.zeros((R, T_MAX + 1), device=dev, dtype=torch.int64)
@@ -80,10 +71,7 @@ class DecodeSession:
         decodes several prompts against one encoder pass, run_pseudo_labelling_v3.py:309-321)."""
         if key is not None and key == self._cross_key:
             return
-        if self.use_enc:  # copied: the engine's encoder buffer is reused by the next encode()
-            self.enc.copy_(enc.reshape(self.enc.shape))
-        else:
-            self.eng.cross_kv(enc, self.B, out=self.cross)
+        self.eng.cross_kv(enc, self.B, out=self.cross)
         self._cross_key = key
 
     def _buffers(self, q: int):
@@ -103,10 +91,6 @@ class DecodeSession:
             )
             if self.eng.packed:  # bf16 mirror of the residual stream (the LayerNorm-fused linears' operand)
                 self._bufs[q]["hb"] = torch.empty((rows, d), device=dev, dtype=torch.bfloat16)
-            if self.use_enc:  # cross-attention queries u = Wk_h^T q_h and values z, [rows][H][d]
-                H = self.eng.H
-                self._bufs[q]["u"] = torch.empty((rows, H * d), device=dev, dtype=dt)
-                self._bufs[q]["z"] = torch.empty((rows, H * d), device=dev, dtype=dt)
         return self._bufs[q]
 
     def _gemm(self, A, W, C, M, N, K, **kw):
@@ -139,14 +123,7 @@ class DecodeSession:
                                tag="o"))
                 seq.append(lin(hb, lay["xq_w"], rows, d, d, ln=(eps, lay["xq_cs"]), bias=lay["xq_b"],
                                C=b["qx"], scale=scale, scale_cols=d, workspace=ws, tag="xq"))
-                if self.use_enc:  # u_h = Wk_h^T q_h -> z_h over the encoder output -> Wv_h z_h + bv
-                    seq.append(lin(b["qx"], lay["xu_w"], rows, H * d, _HD, ldx=d, C=b["u"], x_groups=(d, _HD),
-                                   workspace=ws, tag="xu"))
-                    seq.append(("xenc", q, b["u"], b["z"]))
-                    seq.append(lin(b["z"], lay["xv_w"], rows, d, d, ldx=H * d, bias=lay["xv_b"], C=b["attn"],
-                                   x_groups=(_HD, d), workspace=ws, tag="xv"))
-                else:
-                    seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
+                seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
                 seq.append(lin(b["attn"], lay["xo_w"], rows, d, d, bias=lay["xo_b"], resid=(h, hb, d, 0),
                                workspace=ws, tag="xo"))
                 seq.append(lin(hb, lay["fc1_w"], rows, s.decoder_ffn_dim, d, ln=(eps, lay["fc1_cs"]),
@@ -196,9 +173,6 @@ class DecodeSession:
                 _, q, qkv, li, out = p
                 ops.self_attn_step(qkv, B, q, H, _HD, self.kc[li], self.vc[li], T_MAX, self.cur_len, out, self.self_ws,
                                    bp=self.bp if q == 1 else None)
-            elif k == "xenc":  # rows b*q + i attend to item b's encoder output
-                _, q, u, z = p
-                ops.cross_attn_enc(self.enc, self.B, self.T, s.d_model, u, q, H, z, self.xenc_ws)
             elif k == "cross":  # rows b*nb*q + (beam*q + i) attend to item b's K/V
                 _, q, qx, li, out, ws = p
                 ops.cross_attn_step(qx, self.B, q * self.nb, H, _HD, self.cross[2 * li], self.cross[2 * li + 1],
@@ -249,8 +223,7 @@ class DecodeSession:
         self.counter.zero_()
         self.n_unfinished.fill_(B)
         # the sampler plan, its processor tables and the captured step graph are kept per configuration:
-        # a repeat call (the next batch) replays the same graph -- no re-capture, whose device-wide
-        # synchronize would also wait for an encoder running beside this decode (generate_pipelined)
+        # a repeat call (the next batch) replays the same graph (no re-capture)
         key = (max_length, P, bool(return_timestamps), tuple(gen.suppress_tokens or ()),
                tuple(gen.begin_suppress_tokens or ()), gen.timestamp_begin, gen.no_timestamps_token_id,
                gen.eos_token_id, gen.pad_token_id, gen.max_initial_timestamp_index, bool(record_scores))

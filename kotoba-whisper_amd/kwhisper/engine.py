@@ -10,9 +10,8 @@ Layout in HBM (DESIGN.md §Data layout):
     decoder residual f32 with a bf16 mirror; GEMM inputs (LayerNorm outputs) in the compute dtype;
   * conv stem: mel -> time-major zero-padded [B][3002][c_pad], conv1 output [B][3002][d]
     (pad rows stay zero), so both convolutions are im2col-free GEMMs;
-  * encoder q/k/v head-split [3][B][H][1500][64]; greedy bf16 decoding reads the encoder output [B][1500][d]
-    directly (kw_cross_attn_enc: K/V projections absorbed into the query / value linears); otherwise the
-    cross-attention K/V of all decoder layers from ONE GEMM straight into the static cache [2L][B][H][1500][64];
+  * encoder q/k/v head-split [3][B][H][1500][64]; the cross-attention K/V of all decoder layers from ONE
+    GEMM straight into the static cache [2L][B][H][1500][64];
   * decoder self K/V static cache [L][B][H][448][64]; decode-step weights pre-packed into 1-KB MFMA
     fragments (bf16) for the skinny GEMMs.
 """
@@ -63,12 +62,9 @@ class WhisperEngine:
     """
 
     def __init__(self, shape: WhisperShape, state_dict: dict, *, dtype=torch.bfloat16, device="cuda",
-                 generation_config: GenerationConstants | None = None, cross_attention: str = "kv_cache"):
+                 generation_config: GenerationConstants | None = None):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
-        if cross_attention not in ("kv_cache", "encoder_output"):
-            raise ValueError("cross_attention must be 'kv_cache' or 'encoder_output'")
-        self.cross_attention = cross_attention
         L.load()
         L.load_torch_ops()  # torch.ops.kw.* (the launch path of every op); raises if it was not built
         self.shape = shape
@@ -132,12 +128,6 @@ class WhisperEngine:
         self.dec_pos = self._dev(g("model.decoder.embed_positions.weight"))
         packed = self.dtype == torch.bfloat16
         self.packed = packed
-        # cross_attention="encoder_output" (bf16 engine): greedy decoding reads the encoder output itself (no cross
-        # K/V cache, kw_cross_attn_enc) for the model widths it covers; beam search keeps the K/V cache (beams
-        # share it per item).  Default "kv_cache": at B = 32 on one MI355X the K/V stream measures faster
-        # (kw_cross_attn_enc row)
-        self.xattn_enc = (self.cross_attention == "encoder_output" and packed and d in (384, 512, 768, 1024, 1280)
-                          and self.H <= 32)
         pk = ops.pack_weight if packed else (lambda w: w)
         self.dec_layers = []
         ckv_w, ckv_b = [], []
@@ -173,15 +163,6 @@ class WhisperEngine:
                 fc1_w=fc1_w, fc1_b=fc1_b, fc1_cs=fc1_cs,
                 fc2_w=pk(self._dev(g(f"{p}.fc2.weight"))), fc2_b=self._dev(g(f"{p}.fc2.bias"), f32),
             )
-            if packed and self.xattn_enc:
-                # cross-attention over the encoder output (kw_cross_attn_enc): the K projection moves to the query
-                # side, u_h = Wk_h^T q_h, as a grouped decode linear with W_u[h*d + c][j] = Wk[h*64 + j][c]; the V
-                # projection to the output side, Wv_h z_h + bv (grouped, K = d)
-                wk = g(f"{p}.encoder_attn.k_proj.weight")
-                wu = wk.reshape(self.H, _HD, d).permute(0, 2, 1).reshape(self.H * d, _HD)
-                lay["xu_w"] = pk(self._dev(wu))
-                lay["xv_w"] = pk(self._dev(g(f"{p}.encoder_attn.v_proj.weight")))
-                lay["xv_b"] = self._dev(g(f"{p}.encoder_attn.v_proj.bias"), f32)
             self.dec_layers.append(lay)
             ckv_w += [g(f"{p}.encoder_attn.k_proj.weight"), g(f"{p}.encoder_attn.v_proj.weight")]
             ckv_b += [zero, g(f"{p}.encoder_attn.v_proj.bias")]

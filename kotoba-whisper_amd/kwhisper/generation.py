@@ -81,8 +81,6 @@ class KWhisperForConditionalGeneration:
         self.stats = {}
         self._memo = None  # generate_multitask's per-batch encoder memo
         self._memo_count = 0
-        self._prepared = None  # generate_pipelined: the session slot holding this batch's cross-K/V
-        self._enc_stream = None
 
     # ---- nn.Module-ish surface used by callers ---------------------------------------------------
     @property
@@ -103,11 +101,9 @@ class KWhisperForConditionalGeneration:
         return _Encoder(self.engine)
 
     @classmethod
-    def from_state_dict(cls, shape, state_dict, *, dtype=torch.bfloat16, device="cuda", generation_config=None,
-                        cross_attention="kv_cache"):
+    def from_state_dict(cls, shape, state_dict, *, dtype=torch.bfloat16, device="cuda", generation_config=None):
         shape = PRESETS[shape] if isinstance(shape, str) else shape
-        return cls(WhisperEngine(shape, state_dict, dtype=dtype, device=device, generation_config=generation_config,
-                                 cross_attention=cross_attention))
+        return cls(WhisperEngine(shape, state_dict, dtype=dtype, device=device, generation_config=generation_config))
 
     @classmethod
     def from_pretrained(cls, path_or_name, *, torch_dtype=torch.bfloat16, device="cuda", **kw):
@@ -142,8 +138,8 @@ class KWhisperForConditionalGeneration:
         return cls.from_state_dict(shape, sd, dtype=torch_dtype, device=device, generation_config=gen)
 
     # ---- generate ---------------------------------------------------------------------------------
-    def _session(self, B, beams=1, slot=0):
-        key = (B, beams) if slot == 0 else (B, beams, slot)
+    def _session(self, B, beams=1):
+        key = (B, beams)
         if key not in self._sessions:
             self._sessions[key] = self.engine.new_session(B, beams=beams)
         return self._sessions[key]
@@ -251,11 +247,7 @@ class KWhisperForConditionalGeneration:
                         seg_in[i, :, :n] = feats[p, :, int(seek[p]): int(seek[p]) + n]
                 enc_key = None
                 memo = self._memo
-                prep = self._prepared
-                if prep is not None and whole and passes == 0 and prep["B"] == B and prep["beams"] == num_beams:
-                    # generate_pipelined already ran this batch's encoder + cross-K/V into a session slot
-                    enc, enc_key = None, prep["key"]
-                elif memo is not None and whole and passes == 0:
+                if memo is not None and whole and passes == 0:
                     # multi-task reuse: the first pass of every prompt sees the same mel, so the encoder and
                     # the cross-K/V projection run once per batch (clone: later passes reuse the buffer)
                     if "enc" not in memo:
@@ -274,7 +266,7 @@ class KWhisperForConditionalGeneration:
                 eff_max = max_length
             else:
                 eff_max = P + max_new_tokens
-            sess = self._session(cur, num_beams, prep["slot"] if enc is None else 0)
+            sess = self._session(cur, num_beams)
             sess.set_encoder_output(enc, key=enc_key)
             if num_beams > 1:
                 ids = sess.generate_beam(torch.from_numpy(prompt), gen, num_beams=num_beams, max_length=eff_max,
@@ -329,83 +321,6 @@ class KWhisperForConditionalGeneration:
             return [self.generate(input_features, language=lang, task=task, **kwargs) for lang, task in tasks]
         finally:
             self._memo = None
-
-    def generate_pipelined(self, inputs, *, feature_extractor=None, encoder_cus: int = 64, **kwargs):
-        """``generate(batch, **kwargs)`` for every batch of ``inputs``, yielded in order, with batch i+1's
-        log-mel (if ``feature_extractor`` is given, ``inputs`` are device audio [b, n_samples]), encoder and
-        cross-K/V projection running on CUs [0, encoder_cus) while batch i's decode steps replay on the
-        other CUs (the decode step is latency-bound, the encoder MFMA-bound; disjoint CU sets
-        keep either from starving the other).  A batch with no successor decodes on the whole chip.  The
-        batch loop of run_pseudo_labelling.py:333-344 with the encoder of the next batch overlapped.
-
-        Results are exactly those of calling ``generate`` per batch.  Pipelining applies to the single-pass
-        case (no timestamps, an explicit ``language`` on multilingual models); other settings run batch
-        by batch."""
-        fe = feature_extractor
-        gen = kwargs.get("generation_config") or self.generation_config
-        single_pass = not kwargs.get("return_timestamps") and not getattr(gen, "return_timestamps", False) and \
-            (kwargs.get("language") is not None or not getattr(gen, "lang_to_id", None) or
-             getattr(gen, "language", None) is not None) and "encoder_outputs" not in kwargs
-        feats_of = (lambda x: fe.extract(x)) if fe is not None else (lambda x: x)
-        if not single_pass:
-            for x in inputs:
-                yield self.generate(feats_of(x), **kwargs)
-            return
-        eng = self.engine
-        beams = kwargs.get("num_beams", getattr(gen, "num_beams", None) or 1)
-        if self._enc_stream is None or self._enc_stream[0] != encoder_cus:
-            from . import ops
-
-            ncu = torch.cuda.get_device_properties(eng.device).multi_processor_count
-            self._enc_stream = (encoder_cus, ops.cu_range_stream(0, encoder_cus),
-                                ops.cu_range_stream(encoder_cus, ncu))
-        _, side, dec_stream = self._enc_stream
-        # The CU-masked streams are blocking streams: any operation on the legacy default stream would wait
-        # for them (and they for it), so the loop never touches it -- ``loop`` (non-blocking) orders the
-        # caller's input production, each prepare and each decode.  Outputs are complete when yielded
-        # (generate returns host-synchronised results).
-        loop = torch.cuda.Stream(device=eng.device)
-        loop.wait_stream(torch.cuda.current_stream(eng.device))
-        counter = [0]
-
-        def prepare(x, slot, stream):
-            stream.wait_stream(loop)
-            with torch.cuda.stream(stream):
-                feats = feats_of(x)
-                B = feats.shape[0]
-                counter[0] += 1
-                key = ("pipe", counter[0])
-                self._session(B, beams, slot).set_encoder_output(eng.encode(feats), key=key)
-                done = torch.cuda.Event()
-                done.record(stream)
-            return dict(feats=feats, B=B, beams=beams, slot=slot, key=key, done=done)
-
-        it = iter(inputs)
-        with torch.cuda.stream(loop):
-            try:
-                nxt = prepare(next(it), 1, loop)
-            except StopIteration:
-                return
-        i = 0
-        while nxt is not None:
-            cur = nxt
-            with torch.cuda.stream(loop):
-                loop.wait_event(cur["done"])
-                try:
-                    nxt = prepare(next(it), 1 + (i + 1) % 2, side)  # beside this batch's decode
-                except StopIteration:
-                    nxt = None
-            run_on = loop if nxt is None else dec_stream  # no successor: decode on the whole chip
-            run_on.wait_stream(loop)
-            self._prepared = cur
-            try:
-                with torch.cuda.stream(run_on):
-                    out = self.generate(cur["feats"], **kwargs)
-            finally:
-                self._prepared = None
-            loop.wait_stream(run_on)
-            i += 1
-            yield out
 
     # ---- helpers ------------------------------------------------------------------------------------
     def detect_language(self, input_features=None, encoder_outputs=None, generation_config=None):

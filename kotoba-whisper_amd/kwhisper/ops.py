@@ -71,7 +71,6 @@ def _ws_bytes(kind: str, *dims) -> int:
         return int(_kw().workspace_bytes(kind, [int(d) for d in dims]))
     fn = {"dec_linear": "kw_dec_linear_workspace_bytes", "packed_weight": "kw_packed_weight_bytes",
           "self_attn": "kw_self_attn_workspace", "cross_attn": "kw_cross_attn_workspace",
-          "cross_attn_enc": "kw_cross_attn_enc_workspace",
           "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace"}[kind]
     return int(getattr(_lib(), fn)(*dims))
 
@@ -191,11 +190,10 @@ class DecLinearPlan:
     ``x``: bf16 [M][ldx] activations (x_offset elements from the start); ``ln`` = (eps, colsum f32 [N])
     fuses the LayerNorm of x's rows (gamma/beta folded into W/bias by the caller, colsum = row sums of
     the folded bf16 weight: ``ln_colsum``); STORE writes ``C`` (f32 or bf16, ldc); RESID updates
-    ``resid`` = (h f32, hb bf16 mirror, ldh, row offset); ``x_groups`` = (cols, stride): output column n
-    reads the activations at x + (n // cols) * stride (per-head projections, kw_cross_attn_enc)."""
+    ``resid`` = (h f32, hb bf16 mirror, ldh, row offset)."""
 
     def __init__(self, x, W, M, N, K, *, ldx=None, x_offset=0, ln=None, bias=None, C=None, ldc=None, c_offset=0,
-                 gelu=False, scale=1.0, scale_cols=0, resid=None, workspace=None, x_groups=None, tag=None):
+                 gelu=False, scale=1.0, scale_cols=0, resid=None, workspace=None, tag=None):
         _cuda(x, W, bias, C, workspace)
         self.tag = tag  # a name for per-kernel timing (bench.py), no effect on the call
         if x.dtype != torch.bfloat16 or W.dtype != torch.bfloat16:
@@ -244,8 +242,6 @@ class DecLinearPlan:
         a.scale = float(scale)
         a.scale_cols = scale_cols
         a.M, a.N, a.K = M, N, K
-        gcols, gstride = x_groups if x_groups is not None else (0, 0)
-        a.x_group_cols, a.x_group_stride = gcols, gstride
         need = dec_linear_workspace_bytes(N, K)
         if workspace is None:
             workspace = torch.zeros((need + 3) // 4, device=W.device, dtype=torch.float32)
@@ -256,7 +252,7 @@ class DecLinearPlan:
         a.ws_bytes = workspace.numel() * workspace.element_size()
         self._keep = tuple(keep)
         geo = [x_offset, ldx, 1 if ln is not None else 0, c_offset, 0 if C is None else (ldc or N), int(bool(gelu)),
-               scale_cols, row0, ldh, M, N, K, gcols, gstride]
+               scale_cols, row0, ldh, M, N, K]
         self._targs = (x, W, bias, colsum, C, h, hb, workspace, geo, float(eps), float(scale))
         self.args = a
         self._ref = ctypes.byref(a)
@@ -337,25 +333,6 @@ def cross_attn_step(q, B, q_len, H, hd, k, v, S, out, workspace):
         return
     L.check(_lib().kw_cross_attn_step(_dt(q), _p(q), B, q_len, H, hd, _p(k), _p(v), S, _p(out), _p(workspace),
                                       workspace.numel() * workspace.element_size(), _s()), "kw_cross_attn_step")
-
-
-def cross_attn_enc_workspace_bytes(B, D) -> int:
-    return _ws_bytes("cross_attn_enc", B, D)
-
-
-def cross_attn_enc(enc, B, S, D, u, q_len, H, z, workspace):
-    """z[r][h] = sum_f softmax_f(u[r][h] . enc[b][f]) enc[b][f] for rows r = b*q_len + i (kw_cross_attn_enc):
-    the cross-attention with its K/V projections absorbed into u (= Wk_h^T q_h) and the value linear."""
-    _cuda(enc, u, z, workspace)
-    if enc.dtype != torch.bfloat16 or u.dtype != torch.bfloat16 or z.dtype != torch.bfloat16:
-        raise ValueError("cross_attn_enc takes bf16 enc / u / z")
-    if enc.numel() < B * S * D or u.numel() < B * q_len * H * D or z.numel() < B * q_len * H * D:
-        raise ValueError("cross_attn_enc: enc must hold [B][S][D], u and z [B*q_len][H][D]")
-    if _BACKEND == "torch":
-        _kw().cross_attn_enc(enc, B, S, D, u, q_len, H, z, workspace)
-        return
-    L.check(_lib().kw_cross_attn_enc(_p(enc), B, S, D, _p(u), q_len, H, _p(z), _p(workspace),
-                                     workspace.numel() * workspace.element_size(), _s()), "kw_cross_attn_enc")
 
 
 def beam_logprobs_workspace_bytes(R: int) -> int:
@@ -469,11 +446,3 @@ class BeamStepPlan:
         else:
             L.check(_lib().kw_beam_logprobs(self._ra, _s()), "kw_beam_logprobs")
             L.check(_lib().kw_beam_select(self._rb, _s()), "kw_beam_select")
-
-
-def cu_range_stream(cu_begin: int, cu_end: int) -> torch.cuda.ExternalStream:
-    """A torch stream over a HIP stream restricted to CUs [cu_begin, cu_end) (kw_stream_create_cu_range).
-    The stream lives as long as the process (it is handed to torch as an external stream)."""
-    h = ctypes.c_void_p()
-    L.check(_lib().kw_stream_create_cu_range(int(cu_begin), int(cu_end), ctypes.byref(h)), "kw_stream_create_cu_range")
-    return torch.cuda.ExternalStream(h.value)

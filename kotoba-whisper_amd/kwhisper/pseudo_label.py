@@ -132,10 +132,24 @@ def _round_path(checkpoint_dir: str, si: int) -> str:
     return os.path.join(checkpoint_dir, f"round_{si:06d}.npz")
 
 
+def run_digest(model, **config) -> str:
+    """A stable digest of what decides the labels besides the item plan: the generate kwargs, the output
+    layout options and the model (its architecture name and compute dtype).  A resume with any of them
+    changed would mix two configurations' rounds, so ``plan.json`` records it (sha256 of sorted JSON)."""
+    import hashlib
+    import json
+
+    shape = getattr(getattr(model, "config", None), "shape", None)
+    ident = {"model": getattr(shape, "name", None) or type(model).__name__, "dtype": str(getattr(model, "dtype", ""))}
+    blob = json.dumps({"model": ident, **config}, sort_keys=True, default=repr)
+    return hashlib.sha256(blob.encode()).hexdigest()
+
+
 def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict) -> List[bool]:
     """Which gathered rounds already have a checkpoint file, as rank 0 sees it (broadcast: every rank skips
     the same rounds, so the per-round collectives stay matched).  The directory's ``plan.json`` (items,
-    batch size, world size) must match this run's: the rounds of another plan hold other items."""
+    batch size, world size, and the digest of the generate kwargs / output layout / model) must match this
+    run's: the rounds of another plan hold other items or other labels."""
     if not checkpoint_dir or n_steps == 0:
         return [False] * n_steps
     import json
@@ -178,7 +192,7 @@ def _load_round(checkpoint_dir: str, si: int):
 
 
 def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                checkpoint_dir=None):
+                checkpoint_dir=None, digest=None):
     """Shared DP loop: ``decode(feats)`` -> list of id matrices (one per output column); each is padded
     across ranks and gathered with the file ids (``run_pseudo_labelling.py:336-344``, v3 ``:309-321``).
     With ``checkpoint_dir``, gathered rounds are checkpointed and rounds already on disk are skipped."""
@@ -193,7 +207,8 @@ def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device,
         torch.device("cuda", torch.cuda.current_device()) if dist is not None and dist.get_backend() == "nccl"
         else torch.device("cpu"))
     done = _done_rounds(checkpoint_dir, len(steps), mask_dev,
-                        {"n_items": int(n_items), "batch_size": int(batch_size), "world_size": int(world)})
+                        {"n_items": int(n_items), "batch_size": int(batch_size), "world_size": int(world),
+                         "config_sha256": digest})
     eval_ids: List[int] = []
     cols: Optional[List[List[np.ndarray]]] = None
     for si, idx in enumerate(steps):
@@ -266,8 +281,10 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
         ids = model.generate(feats, **gen_kwargs)
         return [_with_prompt(ids, prompt) if prompt else ids]
 
+    digest = run_digest(model, gen_kwargs=gen_kwargs, pad_token_id=int(pad_token_id),
+                        legacy_prompt_in_output=bool(legacy_prompt_in_output)) if checkpoint_dir else None
     eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                                 checkpoint_dir)
+                                 checkpoint_dir, digest)
     return eval_ids, (cols[0] if cols else [])
 
 
@@ -287,8 +304,10 @@ def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tens
             return model.generate_multitask(feats, tasks, **gen_kwargs)
         return [model.generate(feats, language=lang, task=task, **gen_kwargs) for lang, task in tasks]
 
+    digest = run_digest(model, gen_kwargs=gen_kwargs, pad_token_id=int(pad_token_id),
+                        text_lang_task=[list(t) for t in text_lang_task]) if checkpoint_dir else None
     eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                                 checkpoint_dir)
+                                 checkpoint_dir, digest)
     if not cols:
         cols = [[] for _ in text_lang_task]
     return eval_ids, {t[0]: c for t, c in zip(text_lang_task, cols)}

@@ -155,3 +155,24 @@ def tone_audio(seed: int, n_samples: int = 480000, sr: int = 16000) -> np.ndarra
     x = 0.3 * np.sin(2 * np.pi * (f0 * t + 20.0 * t * t)) + 0.05 * rng.randn(n_samples)
     x[: n_samples // 7] *= 0.01  # a quiet head exercises the max-8 clamp
     return x.astype(np.float32)
+
+
+def reazon_durations(n: int = 1768, seed: int = 0) -> np.ndarray:
+    """Clip durations (s) of a synthetic stand-in for the ReazonSpeech "tiny" shard that BASELINE config 4
+    pseudo-labels, with the shard's statistics (reference misc/data_statistics.json:1: 1,768 clips, mean
+    4.37 s, min 0.62 s, max 21.8 s): gamma-shaped, clipped, rescaled to the mean, extremes present exactly."""
+    rng = np.random.default_rng(seed)
+    d = rng.gamma(2.2, 4.37 / 2.2, n)
+    for _ in range(20):
+        d = np.clip(d * (4.37 / d.mean()), 0.62, 21.8)
+    d[0], d[1] = 0.62, 21.8
+    d *= (4.37 * n - 0.62 - 21.8) / d[2:].sum() if n > 2 else 1.0
+    d[0], d[1] = 0.62, 21.8
+    return np.clip(d, 0.62, 21.8)
+
+
+def reazon_audio(i: int, dur: float, sr: int = 16000) -> np.ndarray:
+    """Clip ``i`` of the config-4 stand-in: ``run_speed_eval.py:14-17`` noise, ``dur`` seconds (the feature
+    extractor zero-pads it to 30 s, feature_extraction_whisper.py:300-307)."""
+    rng = np.random.RandomState(1000 + i)
+    return ((rng.rand(int(dur * sr)) - 0.5) * 2 * 0.007).astype(np.float32)

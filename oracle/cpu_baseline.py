@@ -5,6 +5,11 @@ Times the reference's own hot path on the host cores: transformers 5.15.0
 run_pseudo_labelling.py:338 when no GPU is present; run_speed_eval.py:53-59 uses fp32 on CPU), with
 random weights of the named architecture, ``language="ja", task="transcribe"``, greedy, the same
 max_length.  Timed like run_speed_eval.py:73-78 (warm-up excluded).
+
+Threads (``torch.set_num_threads(os.cpu_count())``): every CPU this process may use --
+``len(os.sched_getaffinity(0))`` -- capped by ``OMP_NUM_THREADS`` when the host sets it.  The GPU box's
+harness sets it to 16, the host-CPU share of one GPU (the node's 256 CPUs serve 8 GPUs' jobs); the count
+used and the node's CPUs are both reported.
 """
 from __future__ import annotations
 
@@ -12,6 +17,18 @@ import os
 import time
 
 import torch
+
+
+def cpu_share() -> int:
+    """CPUs this process may use (affinity), capped by OMP_NUM_THREADS if set."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def hf_cpu_generate_rate(shape, batch: int, max_length: int, threads: int | None = None, seed: int = 0) -> dict:
@@ -25,7 +42,7 @@ def hf_cpu_generate_rate(shape, batch: int, max_length: int, threads: int | None
     from kwhisper.synthetic import dummy_audio
 
     hf_logging.set_verbosity_error()
-    threads = threads or min(16, os.cpu_count() or 1)
+    threads = threads or cpu_share()
     torch.set_num_threads(threads)
     cfg = WhisperConfig(
         vocab_size=shape.vocab_size, num_mel_bins=shape.num_mel_bins, d_model=shape.d_model,

@@ -39,7 +39,12 @@ def test_exports_every_declared_symbol(lib):
 
 
 def test_version(lib):
-    assert lib.kw_version() == 103
+    """The library's version equals the one include/kwhisper.h documents (INTEGRATION.md reads it the same way)."""
+    import re
+
+    with open(os.path.join(ROOT, "include", "kwhisper.h")) as f:
+        want = int(re.search(r"int kw_version\(void\);\s*/\*\s*(\d+)\s*\*/", f.read()).group(1))
+    assert lib.kw_version() == want == 104
 
 
 def _c_layout(struct, fields):

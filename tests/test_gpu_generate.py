@@ -24,12 +24,11 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def _model(shape, dtype, pad=None, cross_attention="kv_cache"):
+def _model(shape, dtype, pad=None):
     from kwhisper.generation import KWhisperForConditionalGeneration
 
     return KWhisperForConditionalGeneration.from_state_dict(
-        shape, synthetic_state_dict(shape, 0), dtype=dtype, generation_config=generation_constants(shape, pad),
-        cross_attention=cross_attention)
+        shape, synthetic_state_dict(shape, 0), dtype=dtype, generation_config=generation_constants(shape, pad))
 
 
 @pytest.fixture(scope="module")
@@ -103,14 +102,10 @@ def test_tiny_fp32_logits(gold, tiny32):
     np.testing.assert_allclose(got, val, atol=1e-3, rtol=0)  # north-star: logits within 1e-3 fp32
 
 
-@pytest.mark.parametrize("cross", ["kv_cache", "encoder_output"])
-def test_tiny_bf16_logits_and_tokens(gold, tiny16, cross):
-    """bf16 tiny: teacher-forced logits and margin-gated greedy tokens (cross="encoder_output": the decode's
-    cross-attention over the encoder output, 4-position prefill as 24 queries in one launch)."""
+def test_tiny_bf16_logits_and_tokens(gold, tiny16):
+    """bf16 tiny: teacher-forced logits and margin-gated greedy tokens."""
     g = gold("tiny_fp32")
     feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
-    if cross != "kv_cache":
-        tiny16 = _model(TINY, torch.bfloat16, cross_attention=cross)
     eng = tiny16.engine
     sess = eng.new_session(feats.shape[0], eng.encode(feats))
     seq = torch.from_numpy(g["greedy_sequences"])
@@ -118,7 +113,7 @@ def test_tiny_bf16_logits_and_tokens(gold, tiny16, cross):
     idx, val = g["greedy_logits_top_idx"], g["greedy_logits_top_val"]
     got = torch.gather(lg[:, : idx.shape[1]], -1, torch.from_numpy(idx.astype(np.int64))).numpy()
     err = np.abs(got - val)
-    print("tiny bf16 (%s) teacher-forced logit err: max %.4f mean %.4f" % (cross, err.max(), err.mean()))
+    print("tiny bf16 teacher-forced logit err: max %.4f mean %.4f" % (err.max(), err.mean()))
     assert err.max() < 0.25 and err.mean() < 0.03   # bf16 weights/activations, f32 accumulation
     toks = tiny16.generate(feats, language="ja", task="transcribe", max_length=128).cpu().numpy()
     want = g["greedy_tokens"]
@@ -146,12 +141,10 @@ def test_large_fp32_bitexact(gold, shape, tag):
     torch.cuda.empty_cache()
 
 
-@pytest.mark.parametrize("cross", ["kv_cache", "encoder_output"])
-def test_large_bf16_vs_reference(gold, cross):
-    """bf16 large-v3 against the fp32 HF fixture; cross="encoder_output" decodes with kw_cross_attn_enc (the
-    cross K/V projections absorbed into the query / value linears) under the same bars."""
+def test_large_bf16_vs_reference(gold):
+    """bf16 large-v3 against the fp32 HF fixture."""
     g = gold("large_v3_fp32")
-    model = _model(LARGE_V3, torch.bfloat16, cross_attention=cross)
+    model = _model(LARGE_V3, torch.bfloat16)
     feats = torch.from_numpy(oracle_features(LARGE_V3, g["cases"])).cuda()
     eng = model.engine
     enc = eng.encode(feats)
@@ -160,13 +153,12 @@ def test_large_bf16_vs_reference(gold, cross):
     print("large-v3 bf16 encoder rel err", rel)
     assert rel < 0.05
     sess = eng.new_session(2, enc)
-    assert sess.use_enc == (cross == "encoder_output")
     seq = torch.from_numpy(g["greedy_sequences"])
     lg = sess.teacher_forced_logits(seq[:, :-1], 4).cpu()
     idx, val = g["greedy_logits_top_idx"], g["greedy_logits_top_val"]
     got = torch.gather(lg[:, : idx.shape[1]], -1, torch.from_numpy(idx.astype(np.int64))).numpy()
     err = np.abs(got - val)
-    print("large-v3 bf16 (%s) teacher-forced logit err: max %.4f mean %.4f" % (cross, err.max(), err.mean()))
+    print("large-v3 bf16 teacher-forced logit err: max %.4f mean %.4f" % (err.max(), err.mean()))
     assert err.max() < 0.35 and err.mean() < 0.03  # the same bars as config 3 at B = 32 (test_gpu_workloads.py)
     del model, sess
     torch.cuda.empty_cache()
@@ -202,28 +194,6 @@ def test_generate_multitask_reuses_encoder(gold, tiny32, ts):
         np.testing.assert_array_equal(a.cpu().numpy(), b.numpy())
     np.testing.assert_array_equal(again.numpy(), want[0].numpy())  # the memo does not leak into plain calls
     assert n_multi == n_separate - (len(tasks) - 1), (n_multi, n_separate)
-
-
-@pytest.mark.parametrize("ts", [False, True])
-def test_generate_pipelined_matches_per_batch(gold, tiny32, ts):
-    """generate_pipelined (next batch's log-mel + encoder + cross-K/V on a CU-restricted stream beside this
-    batch's decode) yields exactly generate() per batch; with timestamps it runs batch by batch."""
-    from kwhisper.feature_extraction import WhisperFeatureExtractor
-    from kwhisper.synthetic import dummy_audio
-
-    fe = WhisperFeatureExtractor(feature_size=TINY.num_mel_bins)
-    audio = [torch.from_numpy(np.stack([dummy_audio(10 * k + i) for i in range(3)])).cuda() for k in range(4)]
-    kw = dict(language="ja", task="transcribe", max_length=32, return_timestamps=ts)
-    want = [tiny32.generate(fe.extract(a), **kw).cpu() for a in audio]
-    got = list(tiny32.generate_pipelined(audio, feature_extractor=fe, encoder_cus=64, **kw))
-    assert len(got) == len(want)
-    for a, b in zip(got, want):
-        np.testing.assert_array_equal(a.cpu().numpy(), b.numpy())
-    feats = [fe.extract(a) for a in audio[:2]]
-    got2 = list(tiny32.generate_pipelined(feats, **kw))  # features in, no extractor
-    for a, b in zip(got2, want[:2]):
-        np.testing.assert_array_equal(a.cpu().numpy(), b.numpy())
-    assert list(tiny32.generate_pipelined([], **kw)) == []
 
 
 def test_tiny_fp32_longform_bitexact(gold, tiny32):

@@ -270,6 +270,25 @@ def test_resume_refuses_another_plan(tmp_path):
         pseudo_label(_StubModel(), _features, 10, batch_size=3, pad_token_id=PAD, checkpoint_dir=ck)
 
 
+@pytest.mark.parametrize("change", ["gen_kwargs", "pad", "model"])
+def test_resume_refuses_another_configuration(tmp_path, change):
+    """Same items / batch / world but other generate kwargs, pad id or model (compute dtype): the old rounds
+    hold other labels, so the rerun refuses them instead of mixing two configurations."""
+    ck = str(tmp_path / "ck")
+    kw = dict(gen_kwargs={"language": "ja", "task": "transcribe", "return_timestamps": True})
+    pseudo_label(_StubModel(), _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=ck, **kw)
+    if change == "gen_kwargs":
+        kw2 = dict(gen_kwargs={"language": "ja", "task": "transcribe", "return_timestamps": False}, pad_token_id=PAD)
+    elif change == "pad":
+        kw2 = dict(kw, pad_token_id=PAD + 1)
+    else:
+        kw2 = dict(kw, pad_token_id=PAD)
+    other = type("_StubBF16", (_StubModel,), {"dtype": "torch.bfloat16"}) if change == "model" else _StubModel
+    with pytest.raises(ValueError, match="another plan"):
+        pseudo_label(other(), _features, 10, batch_size=4, checkpoint_dir=ck, **kw2)
+    pseudo_label(_StubModel(), _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=ck, **kw)  # same: ok
+
+
 def _resume_worker(rank, world, port, n, bs, ck, out_dir, tag):
     import torch.distributed as dist
 

@@ -35,22 +35,15 @@ SR = 16000
 
 
 def reazon_tiny_durations(n: int = 1768, seed: int = 0) -> np.ndarray:
-    """Durations (s) with the shard's statistics (misc/data_statistics.json:1): gamma-shaped, clipped to
-    [0.62, 21.8], rescaled to mean 4.37 s, with the extremes present exactly."""
-    rng = np.random.default_rng(seed)
-    d = rng.gamma(2.2, 4.37 / 2.2, n)
-    for _ in range(20):
-        d = np.clip(d * (4.37 / d.mean()), 0.62, 21.8)
-    d[0], d[1] = 0.62, 21.8
-    d *= (4.37 * n - 0.62 - 21.8) / d[2:].sum() if n > 2 else 1.0
-    d[0], d[1] = 0.62, 21.8
-    return np.clip(d, 0.62, 21.8)
+    from kwhisper.synthetic import reazon_durations
+
+    return reazon_durations(n, seed)
 
 
 def clip_audio(i: int, dur: float) -> np.ndarray:
-    """run_speed_eval.py:14-17 noise, ``dur`` seconds (zero-padded to 30 s by the feature extractor)."""
-    rng = np.random.RandomState(1000 + i)
-    return ((rng.rand(int(dur * SR)) - 0.5) * 2 * 0.007).astype(np.float32)
+    from kwhisper.synthetic import reazon_audio
+
+    return reazon_audio(i, dur, SR)
 
 
 def config4(a, world, rank, dev):

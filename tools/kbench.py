@@ -102,31 +102,6 @@ def main():
             plans.append(ops.DecLinearPlan(hb, W, B, N, K, **kw))
         us = timeit(plans, a.reps)
         res[name] = {"us": round(us, 2), "GBps": round(N * K * 2 / us / 1e3, 1)}
-    # the cross-attention over the encoder output and its two grouped projections (kw_cross_attn_enc path)
-    if want("xu") or want("xv") or want("xenc"):
-        q = torch.randn(B, d, device=dev).bfloat16()
-        u = torch.empty(B, H * d, device=dev, dtype=torch.bfloat16)
-        z = torch.randn(B, H * d, device=dev).bfloat16()
-        out = torch.empty(B, d, device=dev, dtype=torch.bfloat16)
-        if want("xu"):
-            Ws = [ops.pack_weight((torch.randn(H * d, 64, device=dev) / 8).bfloat16()) for _ in range(nl)]
-            plans = [ops.DecLinearPlan(q, W, B, H * d, 64, ldx=d, C=u, x_groups=(d, 64), workspace=ws) for W in Ws]
-            us = timeit(plans, a.reps)
-            res["xu"] = {"us": round(us, 2), "GBps": round(H * d * 64 * 2 / us / 1e3, 1)}
-        if want("xv"):
-            Ws = [ops.pack_weight((torch.randn(d, d, device=dev) / d ** 0.5).bfloat16()) for _ in range(nl)]
-            bias = torch.zeros(d, device=dev)
-            plans = [ops.DecLinearPlan(z, W, B, d, d, ldx=H * d, bias=bias, C=out, x_groups=(64, d), workspace=ws)
-                     for W in Ws]
-            us = timeit(plans, a.reps)
-            res["xv"] = {"us": round(us, 2), "GBps": round(d * d * 2 / us / 1e3, 1)}
-        if want("xenc"):
-            enc = torch.randn(B, S, d, device=dev).bfloat16()
-            u.copy_((torch.randn(B, H * d, device=dev) * 0.08).bfloat16())
-            xws = torch.zeros((ops.cross_attn_enc_workspace_bytes(B, d) + 3) // 4, device=dev)
-            fns = [lambda: ops.cross_attn_enc(enc, B, S, d, u, 1, H, z, xws) for _ in range(nl)]
-            us = timeit(fns, max(1, a.reps // 4))
-            res["xenc"] = {"us": round(us, 2), "GBps": round(B * S * d * 2 / us / 1e3, 1), "note": "same e every launch"}
     # attention kernels
     if not want("cross_attn") and not want("self_attn"):
         print(json.dumps(res))

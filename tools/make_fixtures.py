@@ -257,10 +257,10 @@ def large_b32_fixtures():
     print(f"large_v3_b32 fixtures done in {time.time() - t0:.1f}s {out['greedy_tokens'].shape}")
 
 
-def large_bf16_ref_fixtures(rows=(0, 16)):
+def large_bf16_ref_fixtures(rows=tuple(range(32))):
     """tests/golden/large_v3_bf16ref.npz: the REFERENCE's own bf16 noise floor at config 3.  The reference
     runs its teacher in bfloat16 (run_pseudo_labelling.py:229,338); here the same HF model is cast to bf16 on
-    CPU and run on two of the config-3 clips: its encoder output, its teacher-forced logits on the fp32
+    CPU and run on the 32 config-3 clips (round 2: rows 0 and 16 only): its encoder output, its teacher-forced logits on the fp32
     reference's token sequence (one decoder pass, at the fp32 top-8 ids) and its own greedy tokens.  The
     bf16 engine's tolerances are stated relative to these (tests/test_gpu_workloads.py)."""
     t0 = time.time()
@@ -283,6 +283,71 @@ def large_bf16_ref_fixtures(rows=(0, 16)):
                                         max_length=128).numpy().astype(np.int64)
     np.savez_compressed(os.path.join(GOLD, "large_v3_bf16ref.npz"), **out)
     print(f"large_v3_bf16ref fixtures done in {time.time() - t0:.1f}s")
+
+
+C4_ITEMS = 32
+
+
+def config4_audio(n=C4_ITEMS):
+    """The first ``n`` clips of the config-4 stand-in (kwhisper.synthetic.reazon_durations / reazon_audio)."""
+    durs = S.reazon_durations()[:n]
+    return durs, [S.reazon_audio(i, float(d)) for i, d in enumerate(durs)]
+
+
+def _aligned_margins(segs, P):
+    """Per output token of one row, the top-1 / top-2 margin of the processed scores of the step that produced
+    it.  A row's output is the concatenation over its seek passes of each pass's leading segment tokens
+    (generation_whisper.py:2000-2074 slices segments from the start of the pass's sequence); every segment of
+    one pass shares that pass's ``result`` (its sequences incl. the prompt, and per-step scores)."""
+    groups = []
+    for s in segs:
+        if groups and groups[-1][0] is s["result"]:
+            groups[-1][1].append(s)
+        else:
+            groups.append((s["result"], [s]))
+    margins, toks = [], []
+    for res, ss in groups:
+        n = sum(len(s["tokens"]) for s in ss)
+        gen = res["sequences"][P:]
+        sc = torch.stack(list(res["scores"]), 0).float()  # (steps, V)
+        assert n <= sc.shape[0]
+        assert torch.equal(sc[:n].argmax(-1), gen[:n]), "greedy step != argmax of its scores"
+        top = sc[:n].topk(2, -1).values
+        margins.append((top[:, 0] - top[:, 1]).numpy())
+        toks.append(gen[:n].numpy())
+    return (np.concatenate(margins) if margins else np.zeros(0, np.float32),
+            np.concatenate(toks) if toks else np.zeros(0, np.int64), len(groups))
+
+
+def large_config4_fixtures():
+    """tests/golden/large_v3_ts_b32_fp32.npz: BASELINE config 4's decode at its own teacher --
+    run_pseudo_labelling.py:333-344 with its defaults (return_timestamps True, :99-102; batch 32,
+    script/distil_whisper_v2.0.sh:32; max_label_length 128; ja / transcribe): HF fp32 large-v3 over the first
+    32 clips of the ReazonSpeech-tiny duration stand-in (0.62-21.8 s, zero-padded to 30 s by the feature
+    extractor).  Stores the token matrix, the per-token top-2 margins of the processed scores (aligned to the
+    output through the seek passes), the number of seek passes per row and the segments."""
+    t0 = time.time()
+    durs, audio = config4_audio()
+    fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins)
+    feats = torch.from_numpy(fe(audio, sampling_rate=16000, return_tensors="np")["input_features"])
+    m = hf_model(LARGE_V3)
+    m.generation_config, gc = hf_gen_config(LARGE_V3)
+    kw = dict(language="ja", task="transcribe", return_timestamps=True, max_length=128)
+    res = run_generate(m, feats, return_dict_in_generate=True, output_scores=True, **kw)
+    print(f"  large_v3_ts_b32: generate ({time.time() - t0:.1f}s)")
+    toks = res["sequences"].numpy().astype(np.int64)
+    P = 3  # [sot, ja, transcribe] (timestamps: no notimestamps token, generation_whisper.py:1591-1603)
+    margin = np.full(toks.shape, np.inf, np.float32)
+    passes = np.zeros(len(audio), np.int64)
+    for b, segs in enumerate(res["segments"]):
+        mg, tk, passes[b] = _aligned_margins(segs, P)
+        assert np.array_equal(tk, toks[b, : len(tk)]) and (toks[b, len(tk):] == gc.pad_token_id).all()
+        margin[b, : len(mg)] = mg
+    segs = [[(float(x["start"]), float(x["end"]), len(x["tokens"])) for x in row] for row in res["segments"]]
+    out = {"durations": durs.astype(np.float64), "tokens": toks, "margin": margin, "passes": passes,
+           "segments": np.array(json.dumps(segs)), "max_length": 128}
+    np.savez_compressed(os.path.join(GOLD, "large_v3_ts_b32_fp32.npz"), **out)
+    print(f"large_v3_ts_b32 fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
 
 
 KOTOBA_BEAM_CASES = [("tone", 0), ("dummy", 0), ("tone", 2), ("dummy", 3)]
@@ -434,6 +499,8 @@ def main():
         large_b32_fixtures()
     if not a.skip_large and a.only in (None, "large_bf16ref"):
         large_bf16_ref_fixtures()
+    if not a.skip_large and a.only in (None, "large_c4"):
+        large_config4_fixtures()
     if not a.skip_large and a.only in (None, "kotoba_beam"):
         kotoba_beam_fixtures()
     if a.only in (None, "pipeline"):
