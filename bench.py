@@ -50,7 +50,7 @@ def kernel_source_files() -> list:
     with open(os.path.join(csrc, "Makefile")) as f:
         m = re.search(r"^SRCS\s*:=\s*(.+)$", f.read(), re.M)
     srcs = m.group(1).split()
-    heads = ("kw_common.h", "gemm_common.h", "processors.h")
+    heads = ("kw_common.h", "attn_common.h", "gemm_common.h", "processors.h")
     return [os.path.join(csrc, x) for x in srcs + list(heads)] + [os.path.join(ROOT, "include", "kwhisper.h")]
 
 
@@ -287,7 +287,7 @@ def main(argv=None):
         """Per-kernel device time inside the decode step: the step's launch sequence run eagerly with HIP
         events around every launch (on the launch stream), so each kernel sees the cache state the graph
         replay gives it (the other kernels' weight streams between two cross-attention launches)."""
-        seq = sess._step_plans(1)
+        seq = sess._step_plans(1, fused=sess.fused_last)
         tot, cnt = {}, {}
         for _ in range(passes):
             evs = []

@@ -29,7 +29,7 @@ enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
 enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 
 /* ABI version (major*100 + minor) and the last error message of this thread. */
-int kw_version(void);  /* 104 */
+int kw_version(void);  /* 105 */
 const char* kw_last_error(void);
 
 /* a1 -- log-mel spectrogram.
@@ -156,6 +156,40 @@ int kw_self_attn_step(int dtype, const void* qkv, int64_t B, int64_t q_len, int6
                       const int32_t* bp, int64_t bp_stride, void* out, void* workspace, size_t ws_bytes,
                       kw_stream_t stream);
 size_t kw_self_attn_workspace(int64_t B, int64_t H, int64_t t_max);
+
+/* The self-attention block of one greedy decode step in ONE launch (bf16): the LayerNorm-fused QKV projection
+ * (TF modeling_whisper.py:446,469-471; q * head_dim^-0.5 :309) and the self-attention step over the static
+ * cache with the new key / value appended (:469-480, cache_utils.py:127-145) -- kw_dec_linear(qkv) followed by
+ * kw_self_attn_step(q_len 1), bitwise the same result, without the kernel boundary: the projection's output is
+ * handed to the attention in-launch as 8-byte {bf16 x 2, tag} granules while the cached K/V rows load.
+ *   x: hb [M][ldx] bf16 (the residual mirror; LayerNorm applied as kw_dec_linear's ln); W: packed [3d][d] with
+ *   gamma folded (kw_pack_weight); ln_colsum / bias: [3d] f32; scale multiplies the q columns (< d);
+ *   k_cache / v_cache: one layer's [M][H][t_max][64] bf16; cur_len: L on device (positions [0, L-1) cached,
+ *   L-1 new), L <= 256; out: [M][d] bf16.  M <= 32, d = 64 H, d <= 1280.
+ * workspace >= kw_dec_qkv_self_workspace(M, d) bytes, ZERO-FILLED before first use (every call re-arms it).
+ * kw_dec_qkv_self_supported(): 1 when the projection's workgroups fit on this device at once (the in-launch
+ * hand-off's forward-progress condition); kw_dec_qkv_self returns KW_EUNSUPPORTED otherwise. */
+typedef struct {
+  const void* x;
+  int64_t ldx;
+  float ln_eps;
+  const float* ln_colsum;
+  const void* W;
+  const float* bias;
+  float scale;
+  int64_t M, d, H;
+  void* k_cache;
+  void* v_cache;
+  int64_t t_max;
+  const int32_t* cur_len;
+  void* out;
+  void* workspace;
+  size_t ws_bytes;
+} kw_dec_qkv_self_args;
+
+int kw_dec_qkv_self(const kw_dec_qkv_self_args* args, kw_stream_t stream);
+size_t kw_dec_qkv_self_workspace(int64_t M, int64_t d);
+int kw_dec_qkv_self_supported(int64_t M, int64_t d, int64_t H);
 
 /* Decoder cross-attention against cached encoder K/V [B][H][S][hd] (TF modeling_whisper.py:323-326).
  * q: [B*q_len][H*hd]; out: [B*q_len][H*hd]; S <= 2048; workspace >= kw_cross_attn_workspace(...) bytes and

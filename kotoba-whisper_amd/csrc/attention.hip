@@ -21,7 +21,7 @@
 //   same launch (write-through partials + arrival counter, MI355X_MICROARCH "Valid forms" row 1).
 #include <math.h>
 
-#include "kw_common.h"
+#include "attn_common.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int v2u32;
@@ -33,7 +33,6 @@ __device__ __forceinline__ uint32_t lds_u32(const void* p) {
 
 namespace {
 
-constexpr float LOG2E = 1.4426950408889634f;
 
 __device__ __forceinline__ void glds16(const void* g, char* lds_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
@@ -56,7 +55,6 @@ __device__ __forceinline__ float xor32_sum(float v) {
 // ------------------------------------------------------------------------------------------------
 constexpr int AQ = 128;        // queries per workgroup
 constexpr int AK = 64;         // keys per tile
-constexpr int HD = 64;
 constexpr int TILE_BYTES = AK * HD * 2;  // 8 KB
 constexpr int ATT_LDS = 2 * 2 * TILE_BYTES;  // K,V x 2 stages = 32 KB (O staging reuses it)
 
@@ -383,34 +381,6 @@ __device__ __forceinline__ void attend_rows(const float qv[8], int k0, int k1, K
 // (256 threads = 32 key slots x 8 lanes; lane (slot, sub) holds 16 B of rows slot, slot+32, ...).
 // Returns the chunk's (m, l) to every thread and the unnormalised o[tid] to threads 0..63.
 // ------------------------------------------------------------------------------------------------
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-template <typename T>
-struct Row8 {
-  u32x4 u[sizeof(T) == 2 ? 1 : 2];
-};
-template <typename T>
-__device__ __forceinline__ Row8<T> ld_row8(const T* p) {  // streamed once per step: non-temporal
-  Row8<T> r;
-  r.u[0] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-  if constexpr (sizeof(T) == 4) r.u[1] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + 1);
-  return r;
-}
-template <typename T>
-__device__ __forceinline__ void unpack8(const Row8<T>& r, float v[8]) {
-  if constexpr (sizeof(T) == 2) {
-    const uint32_t w[4] = {r.u[0][0], r.u[0][1], r.u[0][2], r.u[0][3]};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      v[2 * i] = __uint_as_float(w[i] << 16);
-      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
-    }
-  } else {
-    const uint32_t w[8] = {r.u[0][0], r.u[0][1], r.u[0][2], r.u[0][3], r.u[1][0], r.u[1][1], r.u[1][2], r.u[1][3]};
-#pragma unroll
-    for (int i = 0; i < 8; ++i) v[i] = __uint_as_float(w[i]);
-  }
-}
-
 template <typename T, typename KP, typename VP>
 __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, KP kp, VP vp, float (*red)[64],
                                              float* stat, float& m_out, float& l_out, float& o_out) {
@@ -429,6 +399,33 @@ __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, 
 #pragma unroll
   for (int j = 0; j < 8; ++j)
     if (act(j)) vr[j] = ld_row8<T>(vp(min(k0 + slot + 32 * j, k1 - 1), j) + sub * 8);
+  if constexpr (sizeof(T) == 2) {
+    float ql[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ql[i] = qv[i] * LOG2E;
+    u32x4 k4[8], v4[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      k4[j] = kr[j].u[0];
+      v4[j] = vr[j].u[0];
+    }
+    int nj = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) nj += act(j) ? 1 : 0;
+    float mw, lw, acc[8];
+    wave_row_bf16(ql, k4, v4, k0, k1, slot, nj, mw, lw, acc);
+    if (lane < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
+    }
+    if (lane == 0) {
+      stat[wave] = mw;
+      stat[4 + wave] = lw;
+    }
+    __syncthreads();
+    merge_waves_bf16(stat, red, tid, m_out, l_out, o_out);
+    return;
+  }
   float sc[8];
   float mx = -INFINITY;
 #pragma unroll
@@ -517,11 +514,96 @@ __device__ __forceinline__ void publish_and_combine(float* part, int* cnt, int n
 #pragma unroll
   for (int q = 0; q < NSMAX; ++q)
     if (q < ns) {
-      const float f = expf(ms[q] - M);
+      const float f = chunk_scale<T>(ms[q] - M);
       lt = fmaf(ls[q], f, lt);
       ot = fmaf(os[q], f, ot);
     }
   TypeIO<T>::st(out_row + tid, ot / lt);
+}
+
+// Split combine by 8-byte {value, tag} granules (MI355X_MICROARCH price list, "handoff-1to1": one naturally
+// aligned 8-byte {data, tag} written by ONE sc1 store, polled with sc1 loads; untorn on gfx950): the
+// non-final splits of a row write their partial (m, l, o[64]) as granules tagged 1 and leave at once -- no
+// store drain, no arrival counter, no barrier; the final split (blockIdx.y = ns - 1, dispatched after the
+// others) polls the granules, combines in split order with publish_and_combine's arithmetic (bitwise the
+// same result), and re-arms them (tag 0) for the next launch.  A poll that outlasts XG_SPIN_LIMIT rounds
+// (a protocol failure, never expected) raises the error word at err and writes NaN, so the failure is loud.
+template <typename T>
+__device__ __forceinline__ void publish_granules_and_combine(unsigned long long* gr, int ns, int split, float m, float l,
+                                                             float o, T* out_row, int* err) {
+  constexpr int G = HD + 2;
+  const int tid = threadIdx.x;
+  if (split != ns - 1) {
+    unsigned long long* w = gr + (int64_t)split * G;
+    if (tid < HD) put_granule(w + 2 + tid, o);
+    if (tid == 0) {
+      put_granule(w, m);
+      put_granule(w + 1, l);
+    }
+    return;
+  }
+  if (tid >= HD) return;  // one wave combines: lane = output dimension
+  constexpr int NSMAX = 8;
+  float ms[NSMAX], ls[NSMAX], os[NSMAX];
+  bool bad = false;
+  // one round trip per poll: every granule of every other split in flight at once (indices clamped, so the
+  // loads are unconditional and the compiler puts no wait between them), then one check
+  for (int it = 0;; ++it) {
+    unsigned long long x[3 * (NSMAX - 1)];
+#pragma unroll
+    for (int q = 0; q < NSMAX - 1; ++q) {
+      const unsigned long long* gq = gr + min(q, ns - 2) * G;
+      x[3 * q] = peek_granule(gq);
+      x[3 * q + 1] = peek_granule(gq + 1);
+      x[3 * q + 2] = peek_granule(gq + 2 + tid);
+    }
+    bool ready = true;
+#pragma unroll
+    for (int i = 0; i < 3 * (NSMAX - 1); ++i) ready = ready && (x[i] >> 32) == 1ull;
+    if (ready || it >= XG_SPIN_LIMIT) {
+      bad = !ready;
+#pragma unroll
+      for (int q = 0; q < NSMAX - 1; ++q) {
+        ms[q] = ready ? __uint_as_float((uint32_t)x[3 * q]) : __uint_as_float(0x7fc00000u);
+        ls[q] = __uint_as_float((uint32_t)x[3 * q + 1]);
+        os[q] = __uint_as_float((uint32_t)x[3 * q + 2]);
+      }
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+#pragma unroll
+  for (int q = 0; q < NSMAX; ++q)
+    if (q == ns - 1) {
+      ms[q] = m;
+      ls[q] = l;
+      os[q] = o;
+    }
+  float M = -INFINITY;
+#pragma unroll
+  for (int q = 0; q < NSMAX; ++q)
+    if (q < ns) M = fmaxf(M, ms[q]);
+  float lt = 0.f, ot = 0.f;
+#pragma unroll
+  for (int q = 0; q < NSMAX; ++q)
+    if (q < ns) {
+      const float f = chunk_scale<T>(ms[q] - M);
+      lt = fmaf(ls[q], f, lt);
+      ot = fmaf(os[q], f, ot);
+    }
+  TypeIO<T>::st(out_row + tid, ot / lt);
+  if (bad) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // re-arm for the next launch: every value above was consumed by this wave (data dependence), so no
+  // lane can still be polling a granule another lane clears
+#pragma unroll
+  for (int q = 0; q < NSMAX; ++q)
+    if (q < ns - 1) {
+      __hip_atomic_store(gr + q * G + 2 + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (tid == 0) {
+        __hip_atomic_store(gr + q * G, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gr + q * G + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -604,14 +686,16 @@ __global__ __launch_bounds__(256) void cross_attn_kernel(const T* __restrict__ q
 }
 
 // Cross-attention, bf16, one query row per (row, chunk) workgroup -- as cross_attn_kernel, but the chunk's K
-// (XA_DMA >= 1) and V (XA_DMA == 2) rows arrive by LDS-DMA (global_load_lds_dwordx4, non-temporal) instead of
-// register loads (MI355X_MICROARCH "ldsdma-fill": the LDS-DMA stream runs closer to the HBM rate).  Large-v3
-// B = 32 (tools/lab/xa_dma_check.py, one box, two rounds): K by LDS-DMA 44.4-44.6 us vs 45.4-45.6 for register
-// loads; K and V by LDS-DMA 50.3 us (64 KB of LDS per workgroup: 2 per CU instead of 5).  Wave w's DMA instruction j moves keys k0 + 32 j + 8 w + (0..7) (1 KB,
-// lane = (key, 16-B piece)) to LDS piece 4 j + w and each lane reads back exactly its own 16 B, so the score /
-// softmax / value arithmetic is attend_chunk's, operation for operation (results bitwise equal).
+// rows arrive by LDS-DMA (global_load_lds_dwordx4, non-temporal) and V by register loads (r02: 44.4-44.6 us vs
+// 45.4-45.6 for register loads only, 50.3 with V by LDS-DMA too at 2 workgroups per CU).  Wave w's DMA
+// instruction j moves keys k0 + 32 j + 8 w + (0..7) (1 KB, lane = (key, 16-B piece)) to LDS piece 4 j + w and
+// each lane reads back exactly its own 16 B, so the arithmetic is wave_row_bf16's (bitwise the rows of
+// cross_attn_kernel / cross_attn_multi_kernel).  r03 (tools/lab/xa_lab.hip, large-v3 B = 32 over 32 distinct
+// layers): the same grid only STREAMING its bytes reaches 38-40 us (6.1-6.5 TB/s); the softmax work after
+// the loads land costs the rest -- log2-unit scores with per-wave references (no mid-chunk barrier) and DPP
+// sums take ~2 us of it, the granule combine (no store drain / counter round trips) another ~1 us.
 #ifndef KW_XA_DMA
-#define KW_XA_DMA 1  // 0: register loads only (cross_attn_kernel); 2: V by LDS-DMA too (64 KB LDS: slower, 2 WGs/CU)
+#define KW_XA_DMA 1  // 0: register loads only (cross_attn_kernel)
 #endif
 constexpr int XA_DMA = KW_XA_DMA;
 
@@ -637,12 +721,11 @@ __device__ __forceinline__ u32x4 lds_rd16(const char* p) {
 __global__ __launch_bounds__(256) void cross_attn_dma_kernel(const bf16_t* __restrict__ q, int q_len, int H,
                                                              const bf16_t* __restrict__ kc,
                                                              const bf16_t* __restrict__ vc, int S, int chunk,
-                                                             float* __restrict__ ws, int* __restrict__ cnt,
+                                                             unsigned long long* __restrict__ gran, int* __restrict__ err,
                                                              bf16_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) char kv[(XA_DMA == 2 ? 2 : 1) * 32 * 1024];
+  __shared__ __attribute__((aligned(16))) char kv[32 * 1024];
   __shared__ float red[4][64];
   __shared__ float stat[8];
-  __shared__ int last;
   const int row = blockIdx.x, split = blockIdx.y, ns = gridDim.y;
   const int h = row % H, bq = row / H, b = bq / q_len;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -656,83 +739,45 @@ __global__ __launch_bounds__(256) void cross_attn_dma_kernel(const bf16_t* __res
   // every group j is issued (clamped keys: the host guarantees k1 - k0 > 224, so group 7 has valid keys)
 #pragma unroll
   for (int j = 0; j < 8; ++j) glds16_nt(kb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8, kv + (4 * j + wave) * 1024);
-  Row8<bf16_t> vr[8];
-  if constexpr (XA_DMA == 2) {
+  u32x4 vr[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      glds16_nt(vb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8, kv + 32 * 1024 + (4 * j + wave) * 1024);
-  } else {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) vr[j] = ld_row8<bf16_t>(vb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8);
-  }
+  for (int j = 0; j < 8; ++j) vr[j] = ld_row8<bf16_t>(vb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8).u[0];
   asm volatile("s_waitcnt vmcnt(8)" : "+v"(qraw) :: "memory");  // q and this wave's K pieces landed (V may fly)
-  float qv[8];
+  float ql[8];
   {
     Row8<bf16_t> qr;
     qr.u[0] = qraw;
-    unpack8<bf16_t>(qr, qv);
+    unpack8<bf16_t>(qr, ql);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ql[i] *= LOG2E;
   }
-  raw_barrier();
-  Row8<bf16_t> kr[8];
+  // no barrier: each lane reads back only the 16 B its own DMA wrote, complete at the wave's vmcnt
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  u32x4 kr[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) kr[j].u[0] = lds_rd16(kv + (4 * j + wave) * 1024 + lane * 16);
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kr[0].u[0]), "+v"(kr[1].u[0]), "+v"(kr[2].u[0]), "+v"(kr[3].u[0]),
-               "+v"(kr[4].u[0]), "+v"(kr[5].u[0]), "+v"(kr[6].u[0]), "+v"(kr[7].u[0]));
-  float sc[8];
-  float mx = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float kf[8];
-    unpack8<bf16_t>(kr[j], kf);
-    float sj = 0.f;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kf[i], sj);
-    sj = kw_sum8(sj);
-    sc[j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
-    mx = fmaxf(mx, sc[j]);
-  }
-  mx = wave_max(mx);
-  if (lane == 0) stat[wave] = mx;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  raw_barrier();
-  const float m = fmaxf(fmaxf(stat[0], stat[1]), fmaxf(stat[2], stat[3]));
-  if constexpr (XA_DMA == 2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's V pieces (only it reads them)
-    raw_barrier();
-  }
-  if constexpr (XA_DMA == 2) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) vr[j].u[0] = lds_rd16(kv + 32 * 1024 + (4 * j + wave) * 1024 + lane * 16);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vr[0].u[0]), "+v"(vr[1].u[0]), "+v"(vr[2].u[0]), "+v"(vr[3].u[0]),
-                 "+v"(vr[4].u[0]), "+v"(vr[5].u[0]), "+v"(vr[6].u[0]), "+v"(vr[7].u[0]));
-  }
-  float lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[j] - m) : 0.f;
-    lsum += pj;
-    float vv[8];
-    unpack8<bf16_t>(vr[j], vv);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
-  }
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = kw_sum_hi(acc[i]);
-  lsum = wave_sum(lsum) * 0.125f;
+  for (int j = 0; j < 8; ++j) kr[j] = lds_rd16(kv + (4 * j + wave) * 1024 + lane * 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kr[0]), "+v"(kr[1]), "+v"(kr[2]), "+v"(kr[3]), "+v"(kr[4]), "+v"(kr[5]),
+               "+v"(kr[6]), "+v"(kr[7]));
+  float mw, lw, acc[8];
+  wave_row_bf16(ql, kr, vr, k0, k1, slot, 8, mw, lw, acc);
   if (lane < 8) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
   }
-  if (lane == 0) stat[4 + wave] = lsum;
+  if (lane == 0) {
+    stat[wave] = mw;
+    stat[4 + wave] = lw;
+  }
   __syncthreads();
-  const float l = (stat[4] + stat[5]) + (stat[6] + stat[7]);
-  const float o = tid < HD ? (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]) : 0.f;
+  float m, l, o;
+  merge_waves_bf16(stat, red, tid, m, l, o);
   bf16_t* orow = out + (int64_t)bq * H * HD + h * HD;
   if (ns == 1) {
     if (tid < HD) TypeIO<bf16_t>::st(orow + tid, o / l);
     return;
   }
-  publish_and_combine<bf16_t>(ws + (int64_t)row * ns * (HD + 2), cnt + row, ns, split, m, l, o, orow, &last);
+  publish_granules_and_combine<bf16_t>(gran + (int64_t)row * ns * (HD + 2), ns, split, m, l, o, orow, err);
 }
 
 // Cross-attention for several query rows of one item (the prefill's P prompt positions, and the beams of
@@ -746,6 +791,7 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
                                                                int S, int chunk, float* __restrict__ ws,
                                                                int* __restrict__ cnt, T* __restrict__ out) {
   static_assert(QN % 4 == 0 && QN <= 8, "rows in blocks of 4, at most 8 (the beam limit)");
+  static_assert(sizeof(T) == 2, "bf16 rows (wave_row_bf16)");
   __shared__ float red[4][4][64];
   __shared__ float stat[4][8];
   __shared__ int last;
@@ -779,69 +825,41 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
   __builtin_amdgcn_sched_barrier(0);
   // rows in blocks of 4 (one combine thread per (row, dim) per block): the K/V registers stay live
   // across the blocks, so an item's QN rows cost ONE K/V pass
-  float mrow[QN], lrow[QN], orow_acc[QN];
+  constexpr int NB = QN / 4;
+  float mrow[NB], lrow[NB], orow_acc[NB];  // this thread's row (block bk, row tid / 64): m, l, o[lane]
+  u32x4 k4[8], v4[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    k4[j] = kr[j].u[0];
+    v4[j] = vr[j].u[0];
+  }
 #pragma unroll
   for (int r0 = 0; r0 < QN; r0 += 4) {
     if (r0 >= nq) break;
-    float sc[4][8];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (r0 + r >= nq) break;  // (uniform: rows past the group's last are neither computed nor read)
-      float qv[8];
-      unpack8<T>(qr[r0 + r], qv);
-      float mx = -INFINITY;
+      float ql[8];
+      unpack8<T>(qr[r0 + r], ql);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float kv[8];
-        unpack8<T>(kr[j], kv);
-        float sj = 0.f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) sj = fmaf(qv[i], kv[i], sj);
-        sj = kw_sum8(sj);
-        sc[r][j] = (k0 + slot + 32 * j < k1) ? sj : -INFINITY;
-        mx = fmaxf(mx, sc[r][j]);
-      }
-      mx = wave_max(mx);
-      if (lane == 0) stat[r][wave] = mx;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (r0 + r >= nq) break;
-      const float m = fmaxf(fmaxf(stat[r][0], stat[r][1]), fmaxf(stat[r][2], stat[r][3]));
-      mrow[r0 + r] = m;
-      float lsum = 0.f, acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[r][j] - m) : 0.f;
-        lsum += pj;
-        float vv[8];
-        unpack8<T>(vr[j], vv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        acc[i] = kw_sum_hi(acc[i]);
-      }
-      lsum = wave_sum(lsum) * 0.125f;
+      for (int i = 0; i < 8; ++i) ql[i] *= LOG2E;
+      float mw, lw, acc[8];
+      wave_row_bf16(ql, k4, v4, k0, k1, slot, 8, mw, lw, acc);
       if (lane < 8) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) red[r][wave][lane * 8 + i] = acc[i];
       }
-      if (lane == 0) stat[r][4 + wave] = lsum;
+      if (lane == 0) {
+        stat[r][wave] = mw;
+        stat[r][4 + wave] = lw;
+      }
     }
     __syncthreads();
-    // thread (row rr = tid / 64 of this block, dim dd) collects its element
 #pragma unroll
     for (int r = 0; r < 4; ++r)
-      if (r == (tid >> 6)) {
-        lrow[r0 / 4] = (stat[r][4] + stat[r][5]) + (stat[r][6] + stat[r][7]);
-        orow_acc[r0 / 4] = (red[r][0][lane] + red[r][1][lane]) + (red[r][2][lane] + red[r][3][lane]);
-      }
+      if (r == (tid >> 6)) merge_waves_bf16(stat[r], red[r], lane, mrow[r0 / 4], lrow[r0 / 4], orow_acc[r0 / 4]);
     __syncthreads();  // stat / red are rewritten by the next block
   }
-  constexpr int NB = QN / 4;
   const int dd = lane;
   bool last_any = false;
   if (ns > 1) {
@@ -854,11 +872,7 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
         float* w = ws + (int64_t)row * ns * (HD + 2) + (int64_t)split * (HD + 2);
         __hip_atomic_store(w + 2 + dd, orow_acc[bk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (dd == 0) {
-          float mm = 0.f;
-#pragma unroll
-          for (int r = 0; r < QN; ++r)
-            if (r == rr) mm = mrow[r];
-          __hip_atomic_store(w, mm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(w, mrow[bk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(w + 1, lrow[bk], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -904,7 +918,7 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
 #pragma unroll
     for (int qq = 0; qq < NSMAX; ++qq)
       if (qq < ns) {
-        const float f = expf(ms[qq] - M);
+        const float f = chunk_scale<T>(ms[qq] - M);
         lt = fmaf(ls[qq], f, lt);
         ot = fmaf(os[qq], f, ot);
       }
@@ -1255,9 +1269,16 @@ static size_t cross_partials_bytes(int64_t B, int64_t q_len, int64_t H, int64_t 
   return (size_t)(B * q_len * H) * cross_splits(S) * (HD + 2) * sizeof(float);
 }
 
+// workspace: f32 partials [rows][ns][HD+2] | arrival counters [rows] (publish_and_combine kernels) | error word,
+// padded to 64 B | 8-byte granules [rows][ns][HD+2] (cross_attn_dma_kernel); every region zero before first use
+static size_t cross_granule_offset(int64_t B, int64_t q_len, int64_t H, int64_t S) {
+  const size_t head = cross_partials_bytes(B, q_len, H, S) + (size_t)(B * q_len * H) * sizeof(int) + sizeof(int);
+  return (head + 63) & ~(size_t)63;
+}
+
 extern "C" size_t kw_cross_attn_workspace(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S) {
   (void)hd;
-  return cross_partials_bytes(B, q_len, H, S) + (size_t)(B * q_len * H) * sizeof(int);
+  return cross_granule_offset(B, q_len, H, S) + 2 * cross_partials_bytes(B, q_len, H, S);
 }
 
 extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64_t H, int64_t hd,
@@ -1296,7 +1317,9 @@ extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
   } else if (dtype == KW_DT_BF16 && XA_DMA && chunk > 224 && chunk <= 256 && S - (int64_t)(ns - 1) * chunk > 224)
     hipLaunchKernelGGL(cross_attn_dma_kernel, grid, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
-                       (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
+                       (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk,
+                       (unsigned long long*)((char*)workspace + cross_granule_offset(B, q_len, H, S)),
+                       cnt + B * q_len * H, (bf16_t*)out);
   else if (dtype == KW_DT_BF16)
     hipLaunchKernelGGL(cross_attn_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);

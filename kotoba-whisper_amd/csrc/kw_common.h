@@ -99,6 +99,14 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
+// the same butterfly on DPP / permlane (no LDS round trips); a different association than wave_sum
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += kw_dpp<0xB1>(v);
+  v += kw_dpp<0x4E>(v);
+  v += kw_dpp<0x141>(v);
+  v += kw_dpp<0x140>(v);
+  return kw_swap32_sum(kw_swap16_sum(v));
+}
 __device__ __forceinline__ float wave_max(float v) {
   v = fmaxf(v, kw_dpp<0xB1>(v));
   v = fmaxf(v, kw_dpp<0x4E>(v));

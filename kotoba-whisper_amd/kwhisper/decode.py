@@ -54,6 +54,14 @@ class DecodeSession:
         self.lin_ws = torch.zeros(((ws + 3) // 4,), device=dev, dtype=torch.float32) if ws else None
         self.self_ws = torch.zeros((ops.self_attn_workspace_bytes(R, H, T_MAX) + 3) // 4, device=dev,
                                    dtype=torch.float32)
+        # fused self-attention block (kw_dec_qkv_self): greedy rows of the bf16 engine, <= 32 per session, steps
+        # at positions < 256 (decided per generate call); its granule workspace is zeroed once, every launch
+        # re-arms it
+        self.qs_ok = (eng.packed and beams == 1 and eng.fuse_qkv_self and R <= 32
+                      and ops.qkv_self_supported(R, d, H))
+        self.qs_ws = torch.zeros(((ops.qkv_self_workspace_bytes(R, d) + 3) // 4,), device=dev,
+                                 dtype=torch.float32) if self.qs_ok else None
+        self.fused_last = False  # whether the last step plan built / replayed used kw_dec_qkv_self
         self._graph = None
         self._graph_key = None
         self._cross_key = None
@@ -97,10 +105,14 @@ class DecodeSession:
         """f32 parity-mode linear (kw_gemm)."""
         return [ops.GemmPlan(A, W, C, M, N, K, **kw)]
 
-    def _step_plans(self, q: int):
-        """The decoder forward for q new positions per row (q = prompt length for the prefill, 1 after)."""
-        if q in self._plans:
-            return self._plans[q]
+    def _step_plans(self, q: int, fused: bool = False):
+        """The decoder forward for q new positions per row (q = prompt length for the prefill, 1 after).
+        ``fused`` (q == 1): each layer's LayerNorm-fused QKV projection and self-attention step as ONE
+        kw_dec_qkv_self launch (bitwise the two-launch plan) -- for steps at positions < 256 only."""
+        fused = bool(fused and q == 1 and self.qs_ok)
+        key = (q, fused)
+        if key in self._plans:
+            return self._plans[key]
         eng, s = self.eng, self.eng.shape
         b = self._buffers(q)
         d, H, B = s.d_model, eng.H, self.R  # B: running rows
@@ -116,9 +128,14 @@ class DecodeSession:
             lin = ops.DecLinearPlan
             seq = [("embed", q, h, hb)]
             for li, lay in enumerate(eng.dec_layers):
-                seq.append(lin(hb, lay["qkv_w"], rows, 3 * d, d, ln=(eps, lay["qkv_cs"]), bias=lay["qkv_b"],
-                               C=b["qkv"], scale=scale, scale_cols=d, workspace=ws, tag="qkv"))
-                seq.append(("self", q, b["qkv"], li, b["attn"]))
+                if fused:
+                    seq.append(ops.QkvSelfPlan(hb, lay["qkv_w"], rows, d, H, ln=(eps, lay["qkv_cs"]), bias=lay["qkv_b"],
+                                               scale=scale, k_cache=self.kc[li], v_cache=self.vc[li], t_max=T_MAX,
+                                               cur_len=self.cur_len, out=b["attn"], workspace=self.qs_ws))
+                else:
+                    seq.append(lin(hb, lay["qkv_w"], rows, 3 * d, d, ln=(eps, lay["qkv_cs"]), bias=lay["qkv_b"],
+                                   C=b["qkv"], scale=scale, scale_cols=d, workspace=ws, tag="qkv"))
+                    seq.append(("self", q, b["qkv"], li, b["attn"]))
                 seq.append(lin(b["attn"], lay["o_w"], rows, d, d, bias=lay["o_b"], resid=(h, hb, d, 0), workspace=ws,
                                tag="o"))
                 seq.append(lin(hb, lay["xq_w"], rows, d, d, ln=(eps, lay["xq_cs"]), bias=lay["xq_b"],
@@ -133,7 +150,7 @@ class DecodeSession:
             # final LayerNorm (folded into the packed LM head) + proj_out on the last position of every row
             seq.append(lin(hb, eng.lm_w, B, s.vocab_size, d, ldx=q * d, x_offset=(q - 1) * d,
                            ln=(eps, eng.lm_cs), bias=eng.lm_b, C=self.logits, workspace=ws, tag="lm_head"))
-            self._plans[q] = seq
+            self._plans[key] = seq
             return seq
         seq = [("embed", q, b["h"])]
         for li, lay in enumerate(eng.dec_layers):
@@ -154,7 +171,7 @@ class DecodeSession:
         seq.append(("ln", b["h"], eng.dec_ln_g, eng.dec_ln_b, b["x"]))
         # LM head on the last position of every row (proj_out tied to embed_tokens, f32 logits)
         seq += self._gemm(b["x"], eng.lm_w, self.logits, B, s.vocab_size, d, lda=q * d, a_offset=(q - 1) * d)
-        self._plans[q] = seq
+        self._plans[key] = seq
         return seq
 
     def _run(self, seq):
@@ -198,7 +215,7 @@ class DecodeSession:
         out = []
         self._run(self._step_plans(P))
         out.append(self.logits.clone())
-        step = self._step_plans(1)
+        step = self._step_plans(1, fused=T <= 256)
         for t in range(P, T):
             self.cur_len.fill_(t + 1)
             self._run(step)
@@ -274,7 +291,9 @@ class DecodeSession:
             self.scores.append((self.logits.clone(), score_buf.clone()))
         n_steps = max_length - P  # tokens the reference can add at most
         done = 1
-        step_seq = self._step_plans(1)
+        fused = max_length <= 256  # every step's position < 256 (kw_dec_qkv_self's key range)
+        step_seq = self._step_plans(1, fused=fused)
+        self.fused_last = bool(fused and self.qs_ok)
 
         def one_step():
             self._run(step_seq)

@@ -62,13 +62,16 @@ class WhisperEngine:
     """
 
     def __init__(self, shape: WhisperShape, state_dict: dict, *, dtype=torch.bfloat16, device="cuda",
-                 generation_config: GenerationConstants | None = None):
+                 generation_config: GenerationConstants | None = None, fuse_qkv_self: bool = True):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
         L.load()
         L.load_torch_ops()  # torch.ops.kw.* (the launch path of every op); raises if it was not built
         self.shape = shape
         self.dtype = dtype
+        # greedy bf16 decode steps run each layer's QKV projection + self-attention as one kw_dec_qkv_self launch
+        # (bitwise the two-launch plan; False keeps the two launches, e.g. for A/B timing)
+        self.fuse_qkv_self = bool(fuse_qkv_self)
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("WhisperEngine runs on a cuda (HIP) device only")

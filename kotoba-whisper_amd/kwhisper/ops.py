@@ -71,7 +71,8 @@ def _ws_bytes(kind: str, *dims) -> int:
         return int(_kw().workspace_bytes(kind, [int(d) for d in dims]))
     fn = {"dec_linear": "kw_dec_linear_workspace_bytes", "packed_weight": "kw_packed_weight_bytes",
           "self_attn": "kw_self_attn_workspace", "cross_attn": "kw_cross_attn_workspace",
-          "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace"}[kind]
+          "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace",
+          "qkv_self": "kw_dec_qkv_self_workspace"}[kind]
     return int(getattr(_lib(), fn)(*dims))
 
 
@@ -320,6 +321,54 @@ def self_attn_step(qkv, B, q_len, H, hd, k_cache, v_cache, t_max, cur_len, out, 
     L.check(_lib().kw_self_attn_step(_dt(qkv), _p(qkv), B, q_len, H, hd, _p(k_cache), _p(v_cache), t_max,
                                      _p(cur_len), _p(bp), bp.stride(0) if bp is not None else 0, _p(out),
                                      _p(workspace), nb, _s()), "kw_self_attn_step")
+
+
+def qkv_self_workspace_bytes(M, d) -> int:
+    return _ws_bytes("qkv_self", M, d)
+
+
+def qkv_self_supported(M, d, H) -> bool:
+    """Whether kw_dec_qkv_self can run here: its projection workgroups fit on the device at once (the in-launch
+    hand-off's forward-progress condition) and the shape is one it covers (M <= 32, d = 64 H <= 1280)."""
+    return bool(_lib().kw_dec_qkv_self_supported(int(M), int(d), int(H)))
+
+
+class QkvSelfPlan:
+    """A pre-built ``kw_dec_qkv_self`` call: LayerNorm-fused QKV projection + self-attention step of one decode
+    step in one launch (bitwise kw_dec_linear(qkv) followed by kw_self_attn_step).  ``x``: hb [M][ldx] bf16;
+    ``W`` packed (gamma folded), ``ln`` = (eps, colsum [3d]), ``bias`` f32 [3d]; caches one layer's
+    [M][H][t_max][64]; ``cur_len`` device int32 (L <= 256); ``out`` attn [M][d] bf16; ``workspace`` zero-filled
+    (qkv_self_workspace_bytes)."""
+
+    def __init__(self, x, W, M, d, H, *, ln, bias, scale, k_cache, v_cache, t_max, cur_len, out, workspace, ldx=None,
+                 tag="qkv_self"):
+        _cuda(x, W, bias, k_cache, v_cache, cur_len, out, workspace)
+        eps, colsum = ln
+        _cuda(colsum)
+        if x.dtype != torch.bfloat16 or W.dtype != torch.bfloat16 or out.dtype != torch.bfloat16:
+            raise ValueError("kw_dec_qkv_self takes bf16 activations, packed bf16 weights and a bf16 output")
+        ldx = d if ldx is None else ldx
+        if workspace.numel() * workspace.element_size() < qkv_self_workspace_bytes(M, d):
+            raise ValueError("kw_dec_qkv_self workspace too small")
+        self.tag = tag
+        a = L.QkvSelfArgs()
+        a.x, a.ldx, a.ln_eps, a.ln_colsum = x.data_ptr(), ldx, float(eps), colsum.data_ptr()
+        a.W, a.bias, a.scale = W.data_ptr(), bias.data_ptr() if bias is not None else None, float(scale)
+        a.M, a.d, a.H = M, d, H
+        a.k_cache, a.v_cache, a.t_max, a.cur_len = k_cache.data_ptr(), v_cache.data_ptr(), t_max, cur_len.data_ptr()
+        a.out, a.workspace = out.data_ptr(), workspace.data_ptr()
+        a.ws_bytes = workspace.numel() * workspace.element_size()
+        self._a = a
+        self._ref = ctypes.byref(a)
+        self._keep = (x, W, bias, colsum, k_cache, v_cache, cur_len, out, workspace)
+        self._targs = (x, W, bias, colsum, k_cache, v_cache, cur_len, out, workspace, [ldx, M, d, H, t_max],
+                       float(eps), float(scale))
+
+    def __call__(self):
+        if _BACKEND == "torch":
+            _kw().dec_qkv_self(*self._targs)
+        else:
+            L.check(_lib().kw_dec_qkv_self(self._ref, _s()), "kw_dec_qkv_self")
 
 
 def cross_attn_workspace_bytes(B, q_len, H, hd, S) -> int:

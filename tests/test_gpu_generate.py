@@ -268,3 +268,30 @@ def test_torch_ops_trace_under_torch_compile():
     comp = torch.compile(f, fullgraph=True, backend="aot_eager")(qkv, x.clone())
     for a, b in zip(eager, comp):
         assert torch.equal(a, b)
+
+
+def test_fused_qkv_self_generate_bitwise(gold):
+    """The bf16 engine's greedy decode with the fused self-attention block (kw_dec_qkv_self, the default) gives
+    the same tokens and teacher-forced logits, bit for bit, as the two-launch plan (fuse_qkv_self=False)."""
+    from kwhisper.engine import WhisperEngine
+    from kwhisper.generation import KWhisperForConditionalGeneration
+
+    g = gold("tiny_fp32")
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    sd = synthetic_state_dict(TINY, 0)
+
+    def mk(fuse):
+        return KWhisperForConditionalGeneration(WhisperEngine(TINY, sd, dtype=torch.bfloat16,
+                                                              generation_config=generation_constants(TINY),
+                                                              fuse_qkv_self=fuse))
+
+    fused, plain = mk(True), mk(False)
+    for ts in (False, True):
+        a = fused.generate(feats, language="ja", task="transcribe", max_length=64, return_timestamps=ts).cpu()
+        b = plain.generate(feats, language="ja", task="transcribe", max_length=64, return_timestamps=ts).cpu()
+        assert torch.equal(a, b), ts
+    assert fused._sessions[(4, 1)].fused_last and not plain._sessions[(4, 1)].fused_last
+    seq = torch.from_numpy(g["greedy_sequences"])
+    la = fused.engine.new_session(4, fused.engine.encode(feats)).teacher_forced_logits(seq[:, :-1], 4)
+    lb = plain.engine.new_session(4, plain.engine.encode(feats)).teacher_forced_logits(seq[:, :-1], 4)
+    assert torch.equal(la, lb)

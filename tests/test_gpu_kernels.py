@@ -366,6 +366,40 @@ def test_cross_attn_step(dtype, q_len, S):
     ref = (torch.softmax(qq @ k.float().transpose(-1, -2), -1) @ v.float()).permute(0, 2, 1, 3).reshape(B * q_len, d)
     tol = 1e-5 if dtype == torch.float32 else 2e-2
     torch.testing.assert_close(out.float(), ref, atol=tol, rtol=tol)
+    _check_cross_ws_rearmed(ws, B * q_len * H, S)
+
+
+def test_cross_attn_step_b32_repeated():
+    """The bench shape (large-v3 B = 32, 20 heads, 1500 keys), 64 launches on one workspace: every launch equal
+    (the granule combine is deterministic and re-arms itself), close to fp32, workspace left re-armed."""
+    B, H, S, hd = 32, 20, 1500, 64
+    torch.manual_seed(5)
+    k = torch.randn(B, H, S, hd, device="cuda").bfloat16()
+    v = torch.randn(B, H, S, hd, device="cuda").bfloat16()
+    q = (torch.randn(B, H * hd, device="cuda") * 0.3).bfloat16()
+    out = torch.empty(B, H * hd, device="cuda", dtype=torch.bfloat16)
+    ws = torch.zeros(ops.cross_attn_workspace_bytes(B, 1, H, hd, S) // 4 + 1, device="cuda")
+    ops.cross_attn_step(q, B, 1, H, hd, k, v, S, out, ws)
+    first = out.clone()
+    for _ in range(63):
+        ops.cross_attn_step(q, B, 1, H, hd, k, v, S, out, ws)
+    assert torch.equal(out, first)
+    qq = q.float().view(B, 1, H, hd).permute(0, 2, 1, 3)
+    ref = (torch.softmax(qq @ k.float().transpose(-1, -2), -1) @ v.float()).permute(0, 2, 1, 3).reshape(B, H * hd)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    _check_cross_ws_rearmed(ws, B * H, S)
+
+
+def _check_cross_ws_rearmed(ws, rows, S):
+    """Every launch leaves the workspace as it needs the next one: arrival counters 0, the error word 0 (no
+    granule poll timed out), every {value, tag} granule re-armed to 0 by its combining split."""
+    ns = -(-S // 256)
+    part = rows * ns * 66
+    w = ws.view(torch.int32)
+    assert int(w[part: part + rows].abs().sum()) == 0, "arrival counters not reset"
+    assert int(w[part + rows]) == 0, "cross-attention granule poll timed out"
+    g0 = (4 * (part + rows + 1) + 63) // 64 * 16  # granule region, in int32 words
+    assert int(w[g0: g0 + 2 * part].abs().sum()) == 0, "granules not re-armed"
 
 
 @pytest.mark.parametrize("q_len", [2, 3, 4, 5, 8, 13, 20, 32, 45])
@@ -393,6 +427,8 @@ def test_cross_attn_multirow_bitwise(q_len, S):
             assert torch.equal(out.view(B, q_len, d)[:, i], one), i
         else:
             torch.testing.assert_close(out.view(B, q_len, d)[:, i].float(), one.float(), atol=1e-2, rtol=1e-2)
+    _check_cross_ws_rearmed(ws1, B * H, S)
+    _check_cross_ws_rearmed(ws, B * q_len * H, S)
 
 
 # ---------------------------------------------------------------- greedy step (processors + argmax)
@@ -680,3 +716,46 @@ def test_beam_logprobs_split_rows(rt, R, V, k, n_hist, adv):
         res.append((cv.cpu().numpy(), ci.cpu().numpy()))
     np.testing.assert_array_equal(res[0][1], res[1][1])
     np.testing.assert_allclose(res[0][0], res[1][0], rtol=1e-6, atol=1e-5)
+
+
+# ---------------------------------------------------------------- fused QKV projection + self-attention step
+@pytest.mark.parametrize("M,d,H", [(32, 1280, 20), (7, 1280, 20), (1, 384, 6), (32, 384, 6)])
+@pytest.mark.parametrize("L", [1, 5, 33, 128, 200, 256])
+def test_qkv_self_fused_bitwise(M, d, H, L):
+    """kw_dec_qkv_self == kw_dec_linear(qkv, LayerNorm fused, q scaled) then kw_self_attn_step(q_len 1), bit for
+    bit: the attention output and both caches (the new row appended at L - 1), at positions L = 1 (nothing
+    cached) .. 256 (the largest it takes); the workspace comes back re-armed (every granule tag 0, the error
+    word 0), so a second launch on it gives the same result."""
+    torch.manual_seed(M * 1000 + L + d)
+    t_max, eps = 448, 1e-5
+    hb = torch.randn(M, d, device="cuda").bfloat16()
+    W = (torch.randn(3 * d, d, device="cuda") / d ** 0.5).bfloat16()
+    packed, colsum = ops.pack_weight(W), ops.ln_colsum(W)
+    bias = torch.randn(3 * d, device="cuda") * 0.1
+    kc = torch.randn(M, H, t_max, 64, device="cuda").bfloat16()
+    vc = torch.randn(M, H, t_max, 64, device="cuda").bfloat16()
+    cur = torch.tensor([L], dtype=torch.int32, device="cuda")
+    qkv = torch.empty(M, 3 * d, device="cuda", dtype=torch.bfloat16)
+    lws = torch.zeros(ops.dec_linear_workspace_bytes(3 * d, d) // 4 + 1, device="cuda")
+    ops.DecLinearPlan(hb, packed, M, 3 * d, d, ln=(eps, colsum), bias=bias, C=qkv, scale=0.125, scale_cols=d,
+                      workspace=lws)()
+    kc1, vc1 = kc.clone(), vc.clone()
+    out1 = torch.empty(M, d, device="cuda", dtype=torch.bfloat16)
+    sws = torch.zeros(ops.self_attn_workspace_bytes(M, H, t_max) // 4 + 1, device="cuda")
+    ops.self_attn_step(qkv, M, 1, H, 64, kc1, vc1, t_max, cur, out1, sws)
+    assert ops.qkv_self_supported(M, d, H)
+    qws = torch.zeros(ops.qkv_self_workspace_bytes(M, d) // 4 + 1, device="cuda")
+    for rep in range(2):
+        kc2, vc2 = kc.clone(), vc.clone()
+        out2 = torch.full((M, d), 7.0, device="cuda", dtype=torch.bfloat16)
+        ops.QkvSelfPlan(hb, packed, M, d, H, ln=(eps, colsum), bias=bias, scale=0.125, k_cache=kc2, v_cache=vc2,
+                        t_max=t_max, cur_len=cur, out=out2, workspace=qws)()
+        torch.cuda.synchronize()
+        assert int(qws.view(torch.int32).abs().sum()) == 0, "granules not re-armed / a poll timed out"
+        assert torch.equal(out2, out1), (rep, (out2.float() - out1.float()).abs().max().item())
+        assert torch.equal(kc2, kc1) and torch.equal(vc2, vc1), rep
+
+
+def test_qkv_self_rejects_what_it_does_not_cover():
+    assert not ops.qkv_self_supported(33, 1280, 20)  # more rows than one 32-row tile
+    assert not ops.qkv_self_supported(4, 1280, 16)   # head_dim != 64
