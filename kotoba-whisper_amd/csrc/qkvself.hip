@@ -88,14 +88,19 @@ __global__ __launch_bounds__(512) void qkv_self_kernel(QSP p) {
     const int cg = blockIdx.x;
     const int K = d, N = 3 * d;
     const int nkt = K >> 5;
-    const int nsl = QS_WAVES, sl = wave;
-    const int kt0 = (nkt * sl) / nsl, kt1 = (nkt * (sl + 1)) / nsl;
+    // dec_linear's wave count for this K (choose(): 5 k-tiles per wave): waves past it only stage activations
+    const int nwl = (nkt + QS_KTM - 1) / QS_KTM;
+    const bool lin = wave < nwl;
+    const int nsl = nwl, sl = lin ? wave : nwl - 1;
+    const int kt0 = lin ? (nkt * sl) / nsl : 0, kt1 = lin ? (nkt * (sl + 1)) / nsl : 0;
     const int ktl = max(kt1 - 1, kt0);
     const int arow = lane & 15;
     bf16x8 w[QS_KTM], a0[QS_KTM], a1[QS_KTM];
+    if (lin) {
 #pragma unroll
-    for (int u = 0; u < QS_KTM; ++u)
-      w[u] = __builtin_nontemporal_load(p.W + ((int64_t)cg * nkt + min(kt0 + u, ktl)) * 64 + lane);
+      for (int u = 0; u < QS_KTM; ++u)
+        w[u] = __builtin_nontemporal_load(p.W + ((int64_t)cg * nkt + min(kt0 + u, ktl)) * 64 + lane);
+    }
     const int cpr = nkt * 4, cprp = cpr + 1;
     {
       const int ninst = (32 * cprp + 63) / 64;
@@ -156,17 +161,19 @@ __global__ __launch_bounds__(512) void qkv_self_kernel(QSP p) {
         rpart[wave][16 + (lane & 15)][1] = q1[di];
       }
     }
-    red[wave][0][lane] = c0;
-    red[wave][1][lane] = c1;
+    if (lin) {
+      red[wave][0][lane] = c0;
+      red[wave][1][lane] = c1;
+    }
     __syncthreads();
     if (wave == 0) {
-      for (int w2 = 1; w2 < QS_WAVES; ++w2) {
+      for (int w2 = 1; w2 < nwl; ++w2) {
         c0 += red[w2][0][lane];
         c1 += red[w2][1][lane];
       }
       if (lane < 32) {
         float sx = 0.f, sq = 0.f;
-        for (int w2 = 0; w2 < QS_WAVES; ++w2) {
+        for (int w2 = 0; w2 < nwl; ++w2) {
           sx += rpart[w2][lane][0];
           sq += rpart[w2][lane][1];
         }
