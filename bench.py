@@ -308,16 +308,28 @@ def main(argv=None):
     qx = sess._buffers(1)["qx"]
     attn_out = sess._buffers(1)["attn"]
     ws = sess._buffers(1)["ws"]
+    xc_plans = [it for it in sess._step_plans(1, fused=sess.fused_last) if getattr(it, "tag", None) == "xq_cross"]
+    if xc_plans:  # the step's cross-attention is the fused query projection + K/V stream (kw_dec_xq_cross)
+        def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
+            for pl in xc_plans:
+                pl()
 
-    def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
-        for li in range(n_dec):
-            ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[2 * li], sess.cross[2 * li + 1], S, attn_out, ws)
+        cross_kernel = "xq_cross_kernel"
+        d_model = shape.d_model
+        # K + V of one layer (bf16) + the query projection's weights and activation rows, per launch
+        cross_bytes = 2 * B * H * S * hd * 2 + d_model * d_model * 2 + B * d_model * 2
+        cross_note = ("xq_cross_kernel (decoder cross-attention: LayerNorm-fused query projection + the K/V stream "
+                      "in one launch, K by LDS-DMA; one launch per layer; rocprof name)")
+    else:
+        def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
+            for li in range(n_dec):
+                ops.cross_attn_step(qx, B, 1, H, hd, sess.cross[2 * li], sess.cross[2 * li + 1], S, attn_out, ws)
 
-    cross_kernel = "cross_attn_dma_kernel"
+        cross_kernel = "cross_attn_dma_kernel"
+        cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
+        cross_note = ("cross_attn_dma_kernel (decoder cross-attention K/V stream, K by LDS-DMA, one launch per "
+                      "layer; rocprof name)")
     cross_t = time_fn(cross_all_layers, max(1, iters // 4)) / n_dec
-    cross_bytes = 2 * B * H * S * hd * 2  # K + V of one layer, bf16 (algorithmic)
-    cross_note = ("cross_attn_dma_kernel (decoder cross-attention K/V stream, K by LDS-DMA, one launch per layer; "
-                  "rocprof name)")
     feats = fe.extract(audio)
     enc_t = time_fn(lambda: eng.encode(feats), 3)
     step_graph = sess._graph

@@ -29,7 +29,7 @@ enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
 enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 
 /* ABI version (major*100 + minor) and the last error message of this thread. */
-int kw_version(void);  /* 105 */
+int kw_version(void);  /* 106 */
 const char* kw_last_error(void);
 
 /* a1 -- log-mel spectrogram.
@@ -160,15 +160,17 @@ size_t kw_self_attn_workspace(int64_t B, int64_t H, int64_t t_max);
 /* The self-attention block of one greedy decode step in ONE launch (bf16): the LayerNorm-fused QKV projection
  * (TF modeling_whisper.py:446,469-471; q * head_dim^-0.5 :309) and the self-attention step over the static
  * cache with the new key / value appended (:469-480, cache_utils.py:127-145) -- kw_dec_linear(qkv) followed by
- * kw_self_attn_step(q_len 1), bitwise the same result, without the kernel boundary: the projection's output is
+ * kw_self_attn_step(q_len 1) without the kernel boundary (the projection and caches bitwise the same, the
+ * attention output within bf16 rounding: its keys are summed in 16-slot passes): the projection's output is
  * handed to the attention in-launch as 8-byte {bf16 x 2, tag} granules while the cached K/V rows load.
+ * cur_len outside [1, 256] sets the workspace error word and writes NaN.
  *   x: hb [M][ldx] bf16 (the residual mirror; LayerNorm applied as kw_dec_linear's ln); W: packed [3d][d] with
  *   gamma folded (kw_pack_weight); ln_colsum / bias: [3d] f32; scale multiplies the q columns (< d);
  *   k_cache / v_cache: one layer's [M][H][t_max][64] bf16; cur_len: L on device (positions [0, L-1) cached,
  *   L-1 new), L <= 256; out: [M][d] bf16.  M <= 32, d = 64 H, d <= 1280.
  * workspace >= kw_dec_qkv_self_workspace(M, d) bytes, ZERO-FILLED before first use (every call re-arms it).
- * kw_dec_qkv_self_supported(): 1 when the projection's workgroups fit on this device at once (the in-launch
- * hand-off's forward-progress condition); kw_dec_qkv_self returns KW_EUNSUPPORTED otherwise. */
+ * Every in-launch wait is on work dispatched before it (no co-residency assumption: safe beside other work on
+ * the GPU).  kw_dec_qkv_self_supported(): 1 when the shape is covered. */
 typedef struct {
   const void* x;
   int64_t ldx;
@@ -190,6 +192,38 @@ typedef struct {
 int kw_dec_qkv_self(const kw_dec_qkv_self_args* args, kw_stream_t stream);
 size_t kw_dec_qkv_self_workspace(int64_t M, int64_t d);
 int kw_dec_qkv_self_supported(int64_t M, int64_t d, int64_t H);
+
+/* The cross-attention block's query projection and attention step of one greedy decode step in ONE launch
+ * (bf16): the LayerNorm-fused q projection (TF modeling_whisper.py:483; q * head_dim^-0.5 :309) and the
+ * attention over the item's encoder K / V (:323-356) -- kw_dec_linear(xq) followed by kw_cross_attn_step
+ * (q_len 1) without the kernel boundary, bit for bit: the projection hands the query to the attention
+ * in-launch as 8-byte {bf16 x 2, tag} granules while the chunks' K / V streams are already in flight.
+ *   x: hb [M][ldx] bf16; W: packed [d][d] with gamma folded (kw_pack_weight); ln_colsum / bias: [d] f32; scale
+ *   multiplies every column; k / v: one layer's [M][H][S][64] bf16 (item m's K / V); out: [M][d] bf16.
+ *   M <= 32, d = 64 H <= 1280, S such that kw_cross_attn_step's chunks hold 225..256 keys (e.g. 1500).
+ * workspace >= kw_dec_xq_cross_workspace(M, d, H, S) bytes, ZERO-FILLED before first use (every call re-arms
+ * it).  Every in-launch wait is on work dispatched before it (no co-residency assumption: safe beside other
+ * work on the GPU).  kw_dec_xq_cross_supported(): 1 when the shape is covered. */
+typedef struct {
+  const void* x;
+  int64_t ldx;
+  float ln_eps;
+  const float* ln_colsum;
+  const void* W;
+  const float* bias;
+  float scale;
+  int64_t M, d, H;
+  const void* k;
+  const void* v;
+  int64_t S;
+  void* out;
+  void* workspace;
+  size_t ws_bytes;
+} kw_dec_xq_cross_args;
+
+int kw_dec_xq_cross(const kw_dec_xq_cross_args* args, kw_stream_t stream);
+size_t kw_dec_xq_cross_workspace(int64_t M, int64_t d, int64_t H, int64_t S);
+int kw_dec_xq_cross_supported(int64_t M, int64_t d, int64_t H, int64_t S);
 
 /* Decoder cross-attention against cached encoder K/V [B][H][S][hd] (TF modeling_whisper.py:323-326).
  * q: [B*q_len][H*hd]; out: [B*q_len][H*hd]; S <= 2048; workspace >= kw_cross_attn_workspace(...) bytes and

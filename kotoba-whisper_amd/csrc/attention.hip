@@ -22,6 +22,7 @@
 #include <math.h>
 
 #include "attn_common.h"
+#include "decproj.h"
 
 typedef __attribute__((ext_vector_type(4))) short s16x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int v2u32;
@@ -780,6 +781,127 @@ __global__ __launch_bounds__(256) void cross_attn_dma_kernel(const bf16_t* __res
   publish_granules_and_combine<bf16_t>(gran + (int64_t)row * ns * (HD + 2), ns, split, m, l, o, orow, err);
 }
 
+// ------------------------------------------------------------------------------------------------
+// The cross-attention block's query projection and attention step in ONE launch (bf16 engine, q_len 1):
+// the LayerNorm-fused q projection (TF/models/whisper/modeling_whisper.py:483 encoder_attn_layer_norm,
+// :309 q * head_dim^-0.5) and cross_attn_dma_kernel's attention over the item's encoder K/V (:323-356) --
+// what kw_dec_linear(xq) followed by kw_cross_attn_step computes in two launches, bit for bit.
+//
+//  * workgroups [0, n_lin): the query projection, 16 columns each -- dec_linear's arithmetic on 4 waves
+//    (decproj.h: its 8 waves as virtual waves, reduced in the same order), published as 8-byte
+//    {bf16 x 2, tag} granules [M][d/2];
+//  * workgroups [n_lin, n_lin + M H ns): cross_attn_dma_kernel's (row, chunk) work in its dispatch order
+//    (every row's chunk 0 first, the combining last chunk last).  The query's 4 granules per lane are loaded
+//    BEFORE the chunk's K / V stream is issued and checked once the K pieces land: by then the projection
+//    (a few us; the first wave of chunks needs ~10 us to stream its 64 MB) has published, so the K / V stream
+//    does not wait on it.  The row's last chunk re-arms the row's query granules after its combine (every
+//    other chunk of the row has read them: their partials, polled by the combine, depend on them).
+// The projection workgroups wait for nothing and lead the dispatch order; a chunk waits only for them and for
+// earlier chunks of its row (cross_attn_dma_kernel's combine), so every wait is on work dispatched before it
+// -- resident or finished, whatever else shares the GPU (no co-residency assumption).
+// Polls are bounded: a timeout raises the error word and the row's output is NaN.
+struct XQP {
+  const bf16_t* x;
+  int64_t ldx;
+  float ln_eps;
+  const float* ln_colsum;
+  const bf16x8* W;
+  const float* bias;
+  float scale;
+  int M, d, H, n_lin, S, chunk, ns;
+  const bf16_t* kc;
+  const bf16_t* vc;
+  unsigned long long* qg;    // [M][d/2] query granules
+  unsigned long long* gran;  // cross_attn_dma_kernel's chunk-partial granules
+  int* err;
+  bf16_t* out;
+};
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void xq_cross_kernel(XQP p) {
+  __shared__ __attribute__((aligned(16))) char kv[32 * 1024];  // K pieces (chunks) / reduction scratch (projection)
+  __shared__ float red[4][64];
+  __shared__ float stat[8];
+  if ((int)blockIdx.x < p.n_lin) {
+    proj_publish_granules(ProjArgs{p.x, p.ldx, p.M, p.d, p.d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, p.d},
+                          blockIdx.x, kv, p.qg);
+    return;
+  }
+  const int rows = p.M * p.H;
+  const int r = blockIdx.x - p.n_lin;
+  const int row = r % rows, split = r / rows, ns = p.ns;
+  const int h = row % p.H, b = row / p.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
+  const int k0 = split * p.chunk, k1 = min(p.S, k0 + p.chunk);
+  const bf16_t* kb = p.kc + ((int64_t)b * p.H + h) * p.S * HD;
+  const bf16_t* vb = p.vc + ((int64_t)b * p.H + h) * p.S * HD;
+  unsigned long long* qg = p.qg + (int64_t)b * (p.d / 2) + h * 32;
+  // the query's granules first, then every K piece (LDS-DMA) and V row (inline asm for the query loads: hipcc
+  // would otherwise drain the LDS-DMA in flight before their use)
+  unsigned long long g[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(g[i]) : "v"(qg + sub * 4 + i) : "memory");
+#pragma unroll
+  for (int j = 0; j < 8; ++j) glds16_nt(kb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8, kv + (4 * j + wave) * 1024);
+  u32x4 vr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) vr[j] = ld_row8<bf16_t>(vb + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8).u[0];
+  asm volatile("s_waitcnt vmcnt(8)" : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]) :: "memory");  // q + K landed
+  bool ok = ((g[0] & g[1] & g[2] & g[3]) >> 32) == 1ull;
+  for (int it = 0; __builtin_amdgcn_ballot_w64(!ok) != 0; ++it) {  // the projection not yet published: poll
+    if (it >= XG_SPIN_LIMIT) {
+      if (!ok) {
+        __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) g[i] = 0x7fc07fc0ull | (1ull << 32);  // bf16 NaN pairs: the row fails loudly
+        ok = true;
+      }
+      continue;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g[i] = peek_granule(qg + sub * 4 + i);
+    ok = ((g[0] & g[1] & g[2] & g[3]) >> 32) == 1ull;
+  }
+  float ql[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t wq = (uint32_t)g[i];
+    ql[2 * i] = __uint_as_float(wq << 16) * LOG2E;
+    ql[2 * i + 1] = __uint_as_float(wq & 0xffff0000u) * LOG2E;
+  }
+  // no barrier: each lane reads back only the 16 B its own DMA wrote, complete at the wave's vmcnt
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  u32x4 kr[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) kr[j] = lds_rd16(kv + (4 * j + wave) * 1024 + lane * 16);
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(kr[0]), "+v"(kr[1]), "+v"(kr[2]), "+v"(kr[3]), "+v"(kr[4]), "+v"(kr[5]),
+               "+v"(kr[6]), "+v"(kr[7]));
+  float mw, lw, acc[8];
+  wave_row_bf16(ql, kr, vr, k0, k1, slot, 8, mw, lw, acc);
+  if (lane < 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
+  }
+  if (lane == 0) {
+    stat[wave] = mw;
+    stat[4 + wave] = lw;
+  }
+  __syncthreads();
+  float m, l, o;
+  merge_waves_bf16(stat, red, tid, m, l, o);
+  bf16_t* orow = p.out + (int64_t)b * p.d + h * HD;
+  if (ns == 1) {
+    if (tid < HD) TypeIO<bf16_t>::st(orow + tid, o / l);
+  } else {
+    publish_granules_and_combine<bf16_t>(p.gran + (int64_t)row * ns * (HD + 2), ns, split, m, l, o, orow, p.err);
+  }
+  if (split == ns - 1 && tid < 32)  // re-arm the row's query for the next launch (every chunk has read it)
+    __hip_atomic_store(qg + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Cross-attention for several query rows of one item (the prefill's P prompt positions, and the beams of
 // an item, which all read the same encoder K/V): QN rows per workgroup share ONE pass over the chunk's
 // K/V (the one-row kernel above reads it once per row).  Per row the arithmetic is attend_chunk's,
@@ -1326,6 +1448,62 @@ extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q
   else
     hipLaunchKernelGGL(cross_attn_kernel<float>, grid, dim3(256), 0, s, (const float*)q, (int)q_len, (int)H,
                        (const float*)k, (const float*)v, (int)S, chunk, part, cnt, (float*)out);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}
+
+static size_t xq_gran_offset(int64_t M, int64_t H, int64_t S) {
+  return (kw_cross_attn_workspace(M, 1, H, HD, S) + 63) & ~(size_t)63;
+}
+
+static bool xq_shape_ok(int64_t M, int64_t d, int64_t H, int64_t S) {
+  if (!proj_shape_ok(M, d) || H < 1 || d != HD * H || S < 1 || S > 2048) return false;
+  const int ns = cross_splits(S);
+  const int64_t chunk = (S + ns - 1) / ns;
+  return ns >= 1 && chunk > 224 && chunk <= 256 && S - (int64_t)(ns - 1) * chunk > 224;  // cross_attn_dma_kernel's
+}
+
+extern "C" size_t kw_dec_xq_cross_workspace(int64_t M, int64_t d, int64_t H, int64_t S) {
+  if (M < 1 || d < 2 || H < 1 || S < 1) return 0;
+  return xq_gran_offset(M, H, S) + (size_t)M * (size_t)(d / 2) * sizeof(unsigned long long);
+}
+
+extern "C" int kw_dec_xq_cross_supported(int64_t M, int64_t d, int64_t H, int64_t S) {
+  return xq_shape_ok(M, d, H, S) ? 1 : 0;  // (every wait is on earlier-dispatched work: no residency condition)
+}
+
+extern "C" int kw_dec_xq_cross(const kw_dec_xq_cross_args* a, kw_stream_t stream) {
+  if (!a || !a->x || !a->W || !a->ln_colsum || !a->k || !a->v || !a->out || !a->workspace)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_xq_cross: null pointer");
+  if (!xq_shape_ok(a->M, a->d, a->H, a->S) || a->ldx < a->d || a->ldx % 8 || (uintptr_t)a->x % 16)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_xq_cross: M <= 32 rows, d = 64 H <= 1280, 224 < S / chunks <= 256, "
+                                       "ldx % 8 == 0, 16-B aligned x");
+  if (a->ws_bytes < kw_dec_xq_cross_workspace(a->M, a->d, a->H, a->S))
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_xq_cross: needs a zero-filled workspace of kw_dec_xq_cross_workspace()");
+  XQP p;
+  p.x = reinterpret_cast<const bf16_t*>(a->x);
+  p.ldx = a->ldx;
+  p.ln_eps = a->ln_eps;
+  p.ln_colsum = a->ln_colsum;
+  p.W = reinterpret_cast<const bf16x8*>(a->W);
+  p.bias = a->bias;
+  p.scale = a->scale;
+  p.M = (int)a->M;
+  p.d = (int)a->d;
+  p.H = (int)a->H;
+  p.n_lin = (int)(a->d / 16);
+  p.S = (int)a->S;
+  p.ns = cross_splits(a->S);
+  p.chunk = (int)((a->S + p.ns - 1) / p.ns);
+  p.kc = reinterpret_cast<const bf16_t*>(a->k);
+  p.vc = reinterpret_cast<const bf16_t*>(a->v);
+  char* ws = reinterpret_cast<char*>(a->workspace);
+  p.qg = reinterpret_cast<unsigned long long*>(ws + xq_gran_offset(a->M, a->H, a->S));
+  p.gran = reinterpret_cast<unsigned long long*>(ws + cross_granule_offset(a->M, 1, a->H, a->S));
+  p.err = reinterpret_cast<int*>(ws + cross_partials_bytes(a->M, 1, a->H, a->S)) + a->M * a->H;
+  p.out = reinterpret_cast<bf16_t*>(a->out);
+  const int64_t grid = p.n_lin + a->M * a->H * p.ns;
+  hipLaunchKernelGGL(xq_cross_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, p);
   KW_CHECK_LAUNCH();
   return KW_OK;
 }

@@ -216,6 +216,37 @@ void self_attn_step(const Tensor& qkv, int64_t B, int64_t q_len, int64_t H, int6
         w);
 }
 
+// ---- fused decode cross-attention query + step -----------------------------------------------------------
+// dims = [ldx, M, d, H, S]
+void dec_xq_cross(const Tensor& x, const Tensor& W, const optional<Tensor>& bias, const Tensor& ln_colsum,
+                  const Tensor& k, const Tensor& v, Tensor& out, Tensor& workspace, std::vector<int64_t> dims,
+                  double ln_eps, double scale) {
+  const char* w = "kw_dec_xq_cross";
+  dev(x, w), dev(W, w), dev(bias, w), dev(ln_colsum, w), dev(k, w), dev(v, w), dev(out, w), dev(workspace, w);
+  TORCH_CHECK_VALUE(dims.size() == 5, "kw_dec_xq_cross: dims must hold 5 integers");
+  TORCH_CHECK_VALUE(x.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16 &&
+                        out.scalar_type() == at::kBFloat16 && k.scalar_type() == at::kBFloat16 &&
+                        v.scalar_type() == at::kBFloat16,
+                    "kw_dec_xq_cross takes bf16 activations, packed bf16 weights, bf16 K / V and output");
+  kw_dec_xq_cross_args a{};
+  a.x = ptr(x);
+  a.ldx = dims[0];
+  a.ln_eps = (float)ln_eps;
+  a.ln_colsum = ptr<const float>(ln_colsum);
+  a.W = ptr(W);
+  a.bias = optr<const float>(bias);
+  a.scale = (float)scale;
+  a.M = dims[1], a.d = dims[2], a.H = dims[3];
+  a.k = ptr(k);
+  a.v = ptr(v);
+  a.S = dims[4];
+  a.out = ptr(out);
+  a.workspace = ptr(workspace);
+  a.ws_bytes = (size_t)workspace.numel() * workspace.element_size();
+  c10::DeviceGuard g(x.device());
+  check(kw_dec_xq_cross(&a, stream_of(x)), w);
+}
+
 // ---- fused decode self-attention block (LayerNorm-fused QKV projection + self-attention step) ------------
 // dims = [ldx, M, d, H, t_max]
 void dec_qkv_self(const Tensor& x, const Tensor& W, const optional<Tensor>& bias, const Tensor& ln_colsum,
@@ -369,6 +400,7 @@ int64_t workspace_bytes(std::string kind, std::vector<int64_t> d) {
   if (kind == "cross_attn") return (int64_t)kw_cross_attn_workspace(n(0), n(1), n(2), n(3), n(4));
   if (kind == "greedy_step") return (int64_t)kw_greedy_step_workspace(n(0));
   if (kind == "qkv_self") return (int64_t)kw_dec_qkv_self_workspace(n(0), n(1));
+  if (kind == "xq_cross") return (int64_t)kw_dec_xq_cross_workspace(n(0), n(1), n(2), n(3));
   if (kind == "beam_logprobs") return (int64_t)kw_beam_logprobs_workspace(n(0));
   TORCH_CHECK_VALUE(false, "kw::workspace_bytes: unknown kind ", kind);
 }
@@ -394,6 +426,8 @@ TORCH_LIBRARY(kw, m) {
         "int t_max, Tensor cur_len, Tensor(c!) out, Tensor(d!)? workspace, Tensor? bp) -> ()");
   m.def("dec_qkv_self(Tensor x, Tensor W, Tensor? bias, Tensor ln_colsum, Tensor(a!) k_cache, Tensor(b!) v_cache, "
         "Tensor cur_len, Tensor(c!) out, Tensor(d!) workspace, int[] dims, float ln_eps, float scale) -> ()");
+  m.def("dec_xq_cross(Tensor x, Tensor W, Tensor? bias, Tensor ln_colsum, Tensor k, Tensor v, Tensor(a!) out, "
+        "Tensor(b!) workspace, int[] dims, float ln_eps, float scale) -> ()");
   m.def("cross_attn_step(Tensor q, int B, int q_len, int H, int hd, Tensor k, Tensor v, int S, Tensor(a!) out, "
         "Tensor(b!) workspace) -> ()");
   m.def("greedy_step(Tensor(a!) logits, Tensor suppress_mask, Tensor? begin_suppress, Tensor(b!) ids, "
@@ -419,6 +453,7 @@ TORCH_LIBRARY_IMPL(kw, CUDA, m) {
   m.impl("self_attn_step", &self_attn_step);
   m.impl("cross_attn_step", &cross_attn_step);
   m.impl("dec_qkv_self", &dec_qkv_self);
+  m.impl("dec_xq_cross", &dec_xq_cross);
   m.impl("greedy_step", &greedy_step);
   m.impl("beam_logprobs", &beam_logprobs);
   m.impl("beam_select", &beam_select);

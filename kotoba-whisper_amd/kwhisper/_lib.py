@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("KWHISPER_LIB") or os.path.join(os.path.dirname(os.pat
 TORCH_LIB_PATH = os.environ.get("KWHISPER_TORCH_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                       "libkwhisper_torch.so")
 TORCH_OPS = ("log_mel", "mel_to_time_major", "gemm", "dec_linear", "pack_weight", "layernorm", "attention", "embed",
-             "self_attn_step", "dec_qkv_self", "cross_attn_step", "greedy_step", "beam_logprobs", "beam_select")
+             "self_attn_step", "dec_qkv_self", "dec_xq_cross", "cross_attn_step", "greedy_step", "beam_logprobs", "beam_select")
 
 KW_OK, KW_EINVAL, KW_EHIP, KW_EUNSUPPORTED = 0, 1, 2, 3
 KW_DT_F32, KW_DT_BF16 = 0, 1
@@ -60,6 +60,14 @@ class QkvSelfArgs(ctypes.Structure):
         ("x", c_vp), ("ldx", c_i64), ("ln_eps", ctypes.c_float), ("ln_colsum", c_vp), ("W", c_vp), ("bias", c_vp),
         ("scale", ctypes.c_float), ("M", c_i64), ("d", c_i64), ("H", c_i64), ("k_cache", c_vp), ("v_cache", c_vp),
         ("t_max", c_i64), ("cur_len", c_vp), ("out", c_vp), ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
+    ]
+
+
+class XqCrossArgs(ctypes.Structure):
+    _fields_ = [
+        ("x", c_vp), ("ldx", c_i64), ("ln_eps", ctypes.c_float), ("ln_colsum", c_vp), ("W", c_vp), ("bias", c_vp),
+        ("scale", ctypes.c_float), ("M", c_i64), ("d", c_i64), ("H", c_i64), ("k", c_vp), ("v", c_vp),
+        ("S", c_i64), ("out", c_vp), ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
     ]
 
 
@@ -123,6 +131,9 @@ EXPORTS = {
     "kw_dec_qkv_self": (ctypes.c_int, [ctypes.POINTER(QkvSelfArgs), c_vp]),
     "kw_dec_qkv_self_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
     "kw_dec_qkv_self_supported": (ctypes.c_int, [c_i64, c_i64, c_i64]),
+    "kw_dec_xq_cross": (ctypes.c_int, [ctypes.POINTER(XqCrossArgs), c_vp]),
+    "kw_dec_xq_cross_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64]),
+    "kw_dec_xq_cross_supported": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64]),
     "kw_greedy_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), c_vp]),
     "kw_greedy_step_workspace": (ctypes.c_size_t, [c_i64]),
     "kw_beam_logprobs": (ctypes.c_int, [ctypes.POINTER(BeamLogprobsArgs), c_vp]),

@@ -62,6 +62,11 @@ class DecodeSession:
         self.qs_ws = torch.zeros(((ops.qkv_self_workspace_bytes(R, d) + 3) // 4,), device=dev,
                                  dtype=torch.float32) if self.qs_ok else None
         self.fused_last = False  # whether the last step plan built / replayed used kw_dec_qkv_self
+        # fused cross-attention query + step (kw_dec_xq_cross): one query row per item (greedy), any position
+        self.xc_ok = (eng.packed and beams == 1 and eng.fuse_xq_cross and R <= 32
+                      and ops.xq_cross_supported(R, d, H, self.T))
+        self.xc_ws = torch.zeros(((ops.xq_cross_workspace_bytes(R, d, H, self.T) + 3) // 4,), device=dev,
+                                 dtype=torch.float32) if self.xc_ok else None
         self._graph = None
         self._graph_key = None
         self._cross_key = None
@@ -108,7 +113,7 @@ class DecodeSession:
     def _step_plans(self, q: int, fused: bool = False):
         """The decoder forward for q new positions per row (q = prompt length for the prefill, 1 after).
         ``fused`` (q == 1): each layer's LayerNorm-fused QKV projection and self-attention step as ONE
-        kw_dec_qkv_self launch (bitwise the two-launch plan) -- for steps at positions < 256 only."""
+        kw_dec_qkv_self launch (caches bitwise the two-launch plan's, attention within bf16 rounding) -- for steps at positions < 256 only."""
         fused = bool(fused and q == 1 and self.qs_ok)
         key = (q, fused)
         if key in self._plans:
@@ -138,9 +143,14 @@ class DecodeSession:
                     seq.append(("self", q, b["qkv"], li, b["attn"]))
                 seq.append(lin(b["attn"], lay["o_w"], rows, d, d, bias=lay["o_b"], resid=(h, hb, d, 0), workspace=ws,
                                tag="o"))
-                seq.append(lin(hb, lay["xq_w"], rows, d, d, ln=(eps, lay["xq_cs"]), bias=lay["xq_b"],
-                               C=b["qx"], scale=scale, scale_cols=d, workspace=ws, tag="xq"))
-                seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
+                if q == 1 and self.xc_ok:
+                    seq.append(ops.XqCrossPlan(hb, lay["xq_w"], rows, d, H, ln=(eps, lay["xq_cs"]), bias=lay["xq_b"],
+                                               scale=scale, k=self.cross[2 * li], v=self.cross[2 * li + 1], S=self.T,
+                                               out=b["attn"], workspace=self.xc_ws))
+                else:
+                    seq.append(lin(hb, lay["xq_w"], rows, d, d, ln=(eps, lay["xq_cs"]), bias=lay["xq_b"],
+                                   C=b["qx"], scale=scale, scale_cols=d, workspace=ws, tag="xq"))
+                    seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
                 seq.append(lin(b["attn"], lay["xo_w"], rows, d, d, bias=lay["xo_b"], resid=(h, hb, d, 0),
                                workspace=ws, tag="xo"))
                 seq.append(lin(hb, lay["fc1_w"], rows, s.decoder_ffn_dim, d, ln=(eps, lay["fc1_cs"]),

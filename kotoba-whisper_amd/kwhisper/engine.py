@@ -62,7 +62,8 @@ class WhisperEngine:
     """
 
     def __init__(self, shape: WhisperShape, state_dict: dict, *, dtype=torch.bfloat16, device="cuda",
-                 generation_config: GenerationConstants | None = None, fuse_qkv_self: bool = True):
+                 generation_config: GenerationConstants | None = None, fuse_qkv_self: bool = True,
+                 fuse_xq_cross: bool = True):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
         L.load()
@@ -70,8 +71,11 @@ class WhisperEngine:
         self.shape = shape
         self.dtype = dtype
         # greedy bf16 decode steps run each layer's QKV projection + self-attention as one kw_dec_qkv_self launch
-        # (bitwise the two-launch plan; False keeps the two launches, e.g. for A/B timing)
+        # (caches bitwise the two-launch plan's, attention within bf16 rounding; False keeps the two launches)
         self.fuse_qkv_self = bool(fuse_qkv_self)
+        # ... and each layer's cross-attention query projection + cross-attention step as one kw_dec_xq_cross launch
+        # (bitwise the two-launch plan; False keeps the two launches)
+        self.fuse_xq_cross = bool(fuse_xq_cross)
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("WhisperEngine runs on a cuda (HIP) device only")

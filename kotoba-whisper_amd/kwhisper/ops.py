@@ -72,7 +72,7 @@ def _ws_bytes(kind: str, *dims) -> int:
     fn = {"dec_linear": "kw_dec_linear_workspace_bytes", "packed_weight": "kw_packed_weight_bytes",
           "self_attn": "kw_self_attn_workspace", "cross_attn": "kw_cross_attn_workspace",
           "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace",
-          "qkv_self": "kw_dec_qkv_self_workspace"}[kind]
+          "qkv_self": "kw_dec_qkv_self_workspace", "xq_cross": "kw_dec_xq_cross_workspace"}[kind]
     return int(getattr(_lib(), fn)(*dims))
 
 
@@ -328,14 +328,13 @@ def qkv_self_workspace_bytes(M, d) -> int:
 
 
 def qkv_self_supported(M, d, H) -> bool:
-    """Whether kw_dec_qkv_self can run here: its projection workgroups fit on the device at once (the in-launch
-    hand-off's forward-progress condition) and the shape is one it covers (M <= 32, d = 64 H <= 1280)."""
+    """Whether kw_dec_qkv_self covers the shape (M <= 32, d = 64 H <= 1280)."""
     return bool(_lib().kw_dec_qkv_self_supported(int(M), int(d), int(H)))
 
 
 class QkvSelfPlan:
     """A pre-built ``kw_dec_qkv_self`` call: LayerNorm-fused QKV projection + self-attention step of one decode
-    step in one launch (bitwise kw_dec_linear(qkv) followed by kw_self_attn_step).  ``x``: hb [M][ldx] bf16;
+    step in one launch (kw_dec_linear(qkv) then kw_self_attn_step: caches bitwise, attention within bf16 rounding).  ``x``: hb [M][ldx] bf16;
     ``W`` packed (gamma folded), ``ln`` = (eps, colsum [3d]), ``bias`` f32 [3d]; caches one layer's
     [M][H][t_max][64]; ``cur_len`` device int32 (L <= 256); ``out`` attn [M][d] bf16; ``workspace`` zero-filled
     (qkv_self_workspace_bytes)."""
@@ -369,6 +368,51 @@ class QkvSelfPlan:
             _kw().dec_qkv_self(*self._targs)
         else:
             L.check(_lib().kw_dec_qkv_self(self._ref, _s()), "kw_dec_qkv_self")
+
+
+def xq_cross_workspace_bytes(M, d, H, S) -> int:
+    return _ws_bytes("xq_cross", M, d, H, S)
+
+
+def xq_cross_supported(M, d, H, S) -> bool:
+    """Whether kw_dec_xq_cross can run here: the shape is one it covers (M <= 32, d = 64 H <= 1280, S whose
+    chunks hold 225..256 keys)."""
+    return bool(_lib().kw_dec_xq_cross_supported(int(M), int(d), int(H), int(S)))
+
+
+class XqCrossPlan:
+    """A pre-built ``kw_dec_xq_cross`` call: the LayerNorm-fused cross-attention query projection and the
+    cross-attention step (q_len 1) in one launch (bitwise kw_dec_linear(xq) then kw_cross_attn_step).  ``x``: hb [M][ldx] bf16; ``W`` packed (gamma folded), ``ln`` = (eps, colsum [d]), ``bias``
+    f32 [d]; ``k`` / ``v`` one layer's [M][H][S][64]; ``out`` attn [M][d] bf16; ``workspace`` zero-filled
+    (xq_cross_workspace_bytes)."""
+
+    def __init__(self, x, W, M, d, H, *, ln, bias, scale, k, v, S, out, workspace, ldx=None, tag="xq_cross"):
+        _cuda(x, W, bias, k, v, out, workspace)
+        eps, colsum = ln
+        _cuda(colsum)
+        if any(t.dtype != torch.bfloat16 for t in (x, W, k, v, out)):
+            raise ValueError("kw_dec_xq_cross takes bf16 activations, packed bf16 weights, bf16 K / V and output")
+        ldx = d if ldx is None else ldx
+        if workspace.numel() * workspace.element_size() < xq_cross_workspace_bytes(M, d, H, S):
+            raise ValueError("kw_dec_xq_cross workspace too small")
+        self.tag = tag
+        a = L.XqCrossArgs()
+        a.x, a.ldx, a.ln_eps, a.ln_colsum = x.data_ptr(), ldx, float(eps), colsum.data_ptr()
+        a.W, a.bias, a.scale = W.data_ptr(), bias.data_ptr() if bias is not None else None, float(scale)
+        a.M, a.d, a.H = M, d, H
+        a.k, a.v, a.S = k.data_ptr(), v.data_ptr(), S
+        a.out, a.workspace = out.data_ptr(), workspace.data_ptr()
+        a.ws_bytes = workspace.numel() * workspace.element_size()
+        self._a = a
+        self._ref = ctypes.byref(a)
+        self._keep = (x, W, bias, colsum, k, v, out, workspace)
+        self._targs = (x, W, bias, colsum, k, v, out, workspace, [ldx, M, d, H, S], float(eps), float(scale))
+
+    def __call__(self):
+        if _BACKEND == "torch":
+            _kw().dec_xq_cross(*self._targs)
+        else:
+            L.check(_lib().kw_dec_xq_cross(self._ref, _s()), "kw_dec_xq_cross")
 
 
 def cross_attn_workspace_bytes(B, q_len, H, hd, S) -> int:

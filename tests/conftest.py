@@ -17,6 +17,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: minutes of CPU time")
 
 
+def pytest_collection_modifyitems(config, items):
+    """``slow`` tests (the numpy oracle's large-v3 / kotoba-v2 / long-form pins: minutes of single-threaded
+    numpy each) run when selected explicitly (``-m slow``) or with KW_SLOW=1, so the default CPU suite stays
+    within a few minutes.  Their last full run is recorded in profiles/README.md."""
+    if os.environ.get("KW_SLOW") or "slow" in (config.getoption("markexpr") or "").replace("not slow", ""):
+        return
+    skip = pytest.mark.skip(reason="slow oracle pin: run with -m slow or KW_SLOW=1")
+    for it in items:
+        if "slow" in it.keywords:
+            it.add_marker(skip)
+
+
 def gpu_available() -> bool:
     try:
         import torch

@@ -47,7 +47,20 @@ def test_oracle_log_mel_edges(gold, n_mels):
 
 @pytest.fixture(scope="module")
 def tiny():
-    return WhisperNP(synthetic_state_dict(TINY, 0), TINY)
+    """The tiny oracle, its encoder memoised per mel (most tests here encode the same 4 clips; each numpy
+    encode is seconds).  test_oracle_tiny_encoder, the first to ask, runs the real encoder."""
+    m = WhisperNP(synthetic_state_dict(TINY, 0), TINY)
+    encode, memo = m.encode, {}
+
+    def cached(mel):
+        mel = np.asarray(mel, dtype=np.float32)
+        key = (mel.shape, hash(mel.tobytes()))
+        if key not in memo:
+            memo[key] = encode(mel)
+        return memo[key].copy()
+
+    m.encode = cached
+    return m
 
 
 def test_oracle_tiny_encoder(gold, tiny):
@@ -123,6 +136,7 @@ def test_oracle_large_generate(gold, shape, tag):
     np.testing.assert_array_equal(toks, g["greedy_tokens"])
 
 
+@pytest.mark.slow
 def test_oracle_tiny_longform(gold, tiny):
     """Long-form (> 3000 frames) seek loop: batched with an attention mask, and one clip without."""
     from _util import longform_inputs

@@ -1,0 +1,9 @@
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q -k "attn or qkv_self or xq_cross" --timeout 120 --timeout-method thread > gpurun_out/r03k_pytest_attn.log 2>&1 && echo ATTN_OK &&
+timeout -k 10 300 python -u -m pytest tests/test_gpu_generate.py -m gpu -x -q -s -k "fused" --timeout 200 --timeout-method thread > gpurun_out/r03k_pytest_fused.log 2>&1 && echo FUSED_OK &&
+timeout -k 10 400 python bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/r03k_bench.json 2> gpurun_out/r03k_bench.err && cat gpurun_out/r03k_bench.json &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r03k_prof -o r03k -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/r03k_prof.log 2>&1 && echo PROF_OK &&
+timeout -k 10 600 python -u -m pytest tests/test_gpu_workloads.py -m gpu -x -q -s -k "config4" --timeout 300 --timeout-method thread > gpurun_out/r03k_pytest_c4.log 2>&1 && echo C4_OK
