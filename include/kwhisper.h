@@ -29,7 +29,7 @@ enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
 enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 
 /* ABI version (major*100 + minor) and the last error message of this thread. */
-int kw_version(void);  /* 106 */
+int kw_version(void);  /* 107 */
 const char* kw_last_error(void);
 
 /* a1 -- log-mel spectrogram.
@@ -133,7 +133,10 @@ int kw_layernorm_bf16res(void* x, int64_t rows, int64_t dim, const float* gamma,
                          float eps, void* y, int y_dtype, const void* delta, kw_stream_t stream);
 
 /* Encoder self-attention softmax(Q K^T) V (q pre-scaled; TF sdpa_attention.py:79-166, non-causal).
- * qkv: [3][B][H][T][hd] (dtype), out: [B][T][H*hd] (dtype). hd == 64. */
+ * qkv: [3][B][H][T][hd] (dtype), out: [B][T][H*hd] (dtype). hd == 64.  dtype | KW_ATTN_Q_LOG2 (bf16 only):
+ * q also carries log2(e) (scores in log2 units -- the producer folds it into its q scale), which saves the
+ * softmax one multiply-add per score. */
+#define KW_ATTN_Q_LOG2 0x100
 int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, int64_t T, int64_t hd, void* out,
                  kw_stream_t stream);
 

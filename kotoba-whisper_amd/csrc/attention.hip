@@ -59,6 +59,11 @@ constexpr int AK = 64;         // keys per tile
 constexpr int TILE_BYTES = AK * HD * 2;  // 8 KB
 constexpr int ATT_LDS = 2 * 2 * TILE_BYTES;  // K,V x 2 stages = 32 KB (O staging reuses it)
 
+// QL2: q carries log2(e) too (kw_attention's KW_ATTN_Q_LOG2; the QKV GEMM epilogue folds it into the q scale,
+// one bf16 rounding as before): S^T accumulates on top of -m_run (each lane's 16 accumulators are one query's),
+// so the MFMA output is already the exponent and p = exp2(s) is ONE v_exp per score -- the softmax body's
+// per-score VALU work drops from max + fma + exp + add (+ half a cvt) to max3/2 + exp + add (+ half a cvt)
+template <bool QL2>
 __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict__ qkv, int B, int H, int T,
                                                        bf16_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) char smem[ATT_LDS];
@@ -118,10 +123,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
 
     // S^T for 2 key blocks of 32
     f32x16 st[2];
+    const float sinit = QL2 ? (m_run == -INFINITY ? 0.f : -m_run) : 0.f;  // (QL2: relative to the reference)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) st[i][r] = 0.f;
+      for (int r = 0; r < 16; ++r) st[i][r] = sinit;
       const int row = i * 32 + (lane & 31);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -147,33 +153,62 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
 #pragma unroll
       for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[i][r]);
     mx = xor32_max(mx);
-    // deferred rescale: the exponent reference m_run only moves when a score exceeds it by more than
-    // 8 (p <= e^8, exact in f32 and in bf16's range); most tiles skip the O / l rescale entirely
-    const bool bump = mx > m_run + 8.0f;
-    if (__builtin_amdgcn_ballot_w64(bump)) {
-      const float m_new = bump ? mx : m_run;
-      const float alpha = bump ? __builtin_amdgcn_exp2f((m_run - m_new) * LOG2E) : 1.0f;
+    float rs = 0.f;
+    bf16x8 pf[2][2];
+    if constexpr (QL2) {
+      // scores are log2-unit exponents relative to m_run (0 before the first tile); the reference moves only
+      // when one exceeds it by more than 8 / ln 2 (p <= e^8 as below), then this tile is shifted once more
+      const bool bump = m_run == -INFINITY ? true : mx > 11.5415602f;
+      if (__builtin_amdgcn_ballot_w64(bump)) {
+        const float d = bump ? mx : 0.f;  // the reference's move (a lane with no valid key keeps its reference)
+        const float alpha = (bump && m_run != -INFINITY) ? __builtin_amdgcn_exp2f(-d) : 1.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            o[i][r] *= alpha;
+            st[i][r] -= d;
+          }
+        l_run *= alpha;
+        m_run = (m_run == -INFINITY ? 0.f : m_run) + d;
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
-      l_run *= alpha;
-      m_run = m_new;
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float p = __builtin_amdgcn_exp2f(st[i][8 * s + e]);  // raw v_exp_f32, arguments <= 11.5
+            rs += p;
+            pf[i][s][e] = (__bf16)p;
+          }
+    } else {
+      // deferred rescale: the exponent reference m_run only moves when a score exceeds it by more than
+      // 8 (p <= e^8, exact in f32 and in bf16's range); most tiles skip the O / l rescale entirely
+      const bool bump = mx > m_run + 8.0f;
+      if (__builtin_amdgcn_ballot_w64(bump)) {
+        const float m_new = bump ? mx : m_run;
+        const float alpha = bump ? __builtin_amdgcn_exp2f((m_run - m_new) * LOG2E) : 1.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[i][r] *= alpha;
+        l_run *= alpha;
+        m_run = m_new;
+      }
+      const float mneg = -m_run * LOG2E;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            // raw v_exp_f32: arguments are <= 8 * log2(e) and very negative ones may flush to 0
+            const float p = __builtin_amdgcn_exp2f(fmaf(st[i][8 * s + e], LOG2E, mneg));
+            rs += p;
+            pf[i][s][e] = (__bf16)p;
+          }
     }
-    const float mneg = -m_run * LOG2E;
-    float rs = 0.f;
-    bf16x8 pf[2][2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          // raw v_exp_f32: arguments are <= 8 * log2(e) and very negative ones may flush to 0
-          const float p = __builtin_amdgcn_exp2f(fmaf(st[i][8 * s + e], LOG2E, mneg));
-          rs += p;
-          pf[i][s][e] = (__bf16)p;
-        }
     l_run += xor32_sum(rs);
 
     // O^T += V^T P^T ; A operand via ds_read_b64_tr_b16 from the row-major V tile.  The transposed
@@ -521,42 +556,48 @@ __device__ __forceinline__ void publish_and_combine(float* part, int* cnt, int n
     }
   TypeIO<T>::st(out_row + tid, ot / lt);
 }
-
-// Split combine by 8-byte {value, tag} granules (MI355X_MICROARCH price list, "handoff-1to1": one naturally
-// aligned 8-byte {data, tag} written by ONE sc1 store, polled with sc1 loads; untorn on gfx950): the
-// non-final splits of a row write their partial (m, l, o[64]) as granules tagged 1 and leave at once -- no
-// store drain, no arrival counter, no barrier; the final split (blockIdx.y = ns - 1, dispatched after the
-// others) polls the granules, combines in split order with publish_and_combine's arithmetic (bitwise the
-// same result), and re-arms them (tag 0) for the next launch.  A poll that outlasts XG_SPIN_LIMIT rounds
-// (a protocol failure, never expected) raises the error word at err and writes NaN, so the failure is loud.
-template <typename T>
-__device__ __forceinline__ void publish_granules_and_combine(unsigned long long* gr, int ns, int split, float m, float l,
-                                                             float o, T* out_row, int* err) {
-  constexpr int G = HD + 2;
-  const int tid = threadIdx.x;
+// Chunk-partial hand-off of the bf16 one-row cross-attention (cross_attn_dma_kernel, xq_cross_kernel) through
+// 8-byte {data, tag} granules (MI355X_MICROARCH price list, handoff-1to1: one sc1 store each, sc1 polls, untorn),
+// per WAVE: a non-final chunk's waves each publish their own (m_w, l_w, acc_w[64]) -- no barrier, no store
+// drain, no counter -- and leave.  The final chunk (dispatched after the others) folds, wave by wave and in
+// chunk order, every chunk's partial of that wave with fold_begin / fold_value, then merges the four waves with
+// merge_waves_bf16: exactly what cross_attn_row_kernel's waves compute as they stream, so a row's output is
+// bitwise the same whichever kernel the batch size selects.  Granules [ns - 1][4 waves][66]; each is re-armed
+// (tag 0) by its single consumer.  A poll that outlasts XG_SPIN_LIMIT rounds (a protocol failure, never
+// expected) raises the error word and writes NaN, so the failure is loud.
+__device__ __forceinline__ void wave_partials_combine(unsigned long long* gr, int ns, int split, float mw, float lw,
+                                                      const float (&acc)[8], float (*red)[64], float* stat,
+                                                      bf16_t* out_row, int* err) {
+  constexpr int G = HD + 2, NSMAX = 8;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (split != ns - 1) {
-    unsigned long long* w = gr + (int64_t)split * G;
-    if (tid < HD) put_granule(w + 2 + tid, o);
-    if (tid == 0) {
-      put_granule(w, m);
-      put_granule(w + 1, l);
+    unsigned long long* w = gr + ((int64_t)split * 4 + wave) * G;
+    if (lane < 8) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) put_granule(w + 2 + lane * 8 + i, acc[i]);
+    }
+    if (lane == 0) {
+      put_granule(w, mw);
+      put_granule(w + 1, lw);
     }
     return;
   }
-  if (tid >= HD) return;  // one wave combines: lane = output dimension
-  constexpr int NSMAX = 8;
-  float ms[NSMAX], ls[NSMAX], os[NSMAX];
+  if (lane < 8) {  // this chunk's own partial of dim d = lane*8 + i, read back by lane d of the same wave
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
+  }
+  // lane d of wave w: every earlier chunk's (m, l, acc[d]) of wave w in flight at once (indices clamped: the
+  // loads are unconditional, one round trip), then one check
+  float ms[NSMAX - 1], ls[NSMAX - 1], as[NSMAX - 1];
   bool bad = false;
-  // one round trip per poll: every granule of every other split in flight at once (indices clamped, so the
-  // loads are unconditional and the compiler puts no wait between them), then one check
-  for (int it = 0;; ++it) {
+  for (int it = 0; ns > 1; ++it) {
     unsigned long long x[3 * (NSMAX - 1)];
 #pragma unroll
     for (int q = 0; q < NSMAX - 1; ++q) {
-      const unsigned long long* gq = gr + min(q, ns - 2) * G;
+      const unsigned long long* gq = gr + ((int64_t)min(q, ns - 2) * 4 + wave) * G;
       x[3 * q] = peek_granule(gq);
       x[3 * q + 1] = peek_granule(gq + 1);
-      x[3 * q + 2] = peek_granule(gq + 2 + tid);
+      x[3 * q + 2] = peek_granule(gq + 2 + lane);
     }
     bool ready = true;
 #pragma unroll
@@ -567,44 +608,47 @@ __device__ __forceinline__ void publish_granules_and_combine(unsigned long long*
       for (int q = 0; q < NSMAX - 1; ++q) {
         ms[q] = ready ? __uint_as_float((uint32_t)x[3 * q]) : __uint_as_float(0x7fc00000u);
         ls[q] = __uint_as_float((uint32_t)x[3 * q + 1]);
-        os[q] = __uint_as_float((uint32_t)x[3 * q + 2]);
+        as[q] = __uint_as_float((uint32_t)x[3 * q + 2]);
       }
       break;
     }
     __builtin_amdgcn_s_sleep(1);
   }
+  float M = -INFINITY, Lr = 0.f, A = 0.f;
 #pragma unroll
-  for (int q = 0; q < NSMAX; ++q)
-    if (q == ns - 1) {
-      ms[q] = m;
-      ls[q] = l;
-      os[q] = o;
-    }
-  float M = -INFINITY;
-#pragma unroll
-  for (int q = 0; q < NSMAX; ++q)
-    if (q < ns) M = fmaxf(M, ms[q]);
-  float lt = 0.f, ot = 0.f;
-#pragma unroll
-  for (int q = 0; q < NSMAX; ++q)
-    if (q < ns) {
-      const float f = chunk_scale<T>(ms[q] - M);
-      lt = fmaf(ls[q], f, lt);
-      ot = fmaf(os[q], f, ot);
-    }
-  TypeIO<T>::st(out_row + tid, ot / lt);
+  for (int q = 0; q < NSMAX; ++q) {
+    if (q >= ns) break;
+    float f0 = 0.f, f1 = 0.f;
+    const bool own = q == ns - 1;
+    const float a = own ? red[wave][lane] : as[q < NSMAX - 1 ? q : 0];
+    const int mode = own ? fold_begin(mw, lw, M, Lr, f0, f1) : fold_begin(ms[q < NSMAX - 1 ? q : 0],
+                                                                          ls[q < NSMAX - 1 ? q : 0], M, Lr, f0, f1);
+    A = fold_value(mode, A, a, f0, f1);
+  }
   if (bad) __hip_atomic_store(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // re-arm for the next launch: every value above was consumed by this wave (data dependence), so no
-  // lane can still be polling a granule another lane clears
+  // re-arm for the next launch: every value above was consumed by this lane (data dependence)
 #pragma unroll
-  for (int q = 0; q < NSMAX; ++q)
+  for (int q = 0; q < NSMAX - 1; ++q)
     if (q < ns - 1) {
-      __hip_atomic_store(gr + q * G + 2 + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (tid == 0) {
-        __hip_atomic_store(gr + q * G, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gr + q * G + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned long long* gq = gr + ((int64_t)q * 4 + wave) * G;
+      __hip_atomic_store(gq + 2 + lane, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0) {
+        __hip_atomic_store(gq, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gq + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
+  __syncthreads();  // every wave has read its own red[] row: reuse red / stat for the folded partials
+  red[wave][lane] = A;
+  if (lane == 0) {
+    stat[wave] = M;
+    stat[4 + wave] = Lr;
+  }
+  __syncthreads();
+  if (tid < HD) {
+    float m, l, o;
+    merge_waves_bf16(stat, red, tid, m, l, o);
+    TypeIO<bf16_t>::st(out_row + tid, o / l);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -762,23 +806,8 @@ __global__ __launch_bounds__(256) void cross_attn_dma_kernel(const bf16_t* __res
                "+v"(kr[6]), "+v"(kr[7]));
   float mw, lw, acc[8];
   wave_row_bf16(ql, kr, vr, k0, k1, slot, 8, mw, lw, acc);
-  if (lane < 8) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
-  }
-  if (lane == 0) {
-    stat[wave] = mw;
-    stat[4 + wave] = lw;
-  }
-  __syncthreads();
-  float m, l, o;
-  merge_waves_bf16(stat, red, tid, m, l, o);
-  bf16_t* orow = out + (int64_t)bq * H * HD + h * HD;
-  if (ns == 1) {
-    if (tid < HD) TypeIO<bf16_t>::st(orow + tid, o / l);
-    return;
-  }
-  publish_granules_and_combine<bf16_t>(gran + (int64_t)row * ns * (HD + 2), ns, split, m, l, o, orow, err);
+  wave_partials_combine(gran + (int64_t)row * ns * 4 * (HD + 2), ns, split, mw, lw, acc, red, stat,
+                        out + (int64_t)bq * H * HD + h * HD, err);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -881,25 +910,149 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void x
                "+v"(kr[6]), "+v"(kr[7]));
   float mw, lw, acc[8];
   wave_row_bf16(ql, kr, vr, k0, k1, slot, 8, mw, lw, acc);
+  wave_partials_combine(p.gran + (int64_t)row * ns * 4 * (HD + 2), ns, split, mw, lw, acc, red, stat,
+                        p.out + (int64_t)b * p.d + h * HD, p.err);
+  if (split == ns - 1 && tid < 32)  // re-arm the row's query for the next launch (every chunk has read it)
+    __hip_atomic_store(qg + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Cross-attention, bf16, q_len 1, ONE workgroup per (row, head) pair looping over the pair's chunks with the
+// next chunk's K / V in flight while the current one is computed -- used when every pair fits on the device
+// at once (large-v3 B = 32: 640 workgroups, 3 per CU).  The chunk-per-workgroup grid (cross_attn_dma_kernel)
+// streams in rounds: every workgroup of a round lands its last byte at about the same time, then computes
+// while the memory system idles (tools/lab/xa_lab.hip: the same grid only streaming is 38-40 us, with the
+// softmax 44-46).  Here each wave keeps its own running softmax over the pair's chunks (log2-unit scores,
+// wave_row_bf16, merged online with exp2 rescales); the four waves merge once at the end -- no chunk
+// partials, no combine, no workspace.  With QG the query comes from xq_cross's granules (projection
+// workgroups [0, n_lin) first, as xq_cross_kernel) and the pair re-arms them after use.
+struct CRP {
+  const bf16_t* q;           // [rows][64] (row stride d) when !QG
+  unsigned long long* qg;    // [M][d/2] query granules when QG
+  const bf16_t* kc;
+  const bf16_t* vc;
+  int H, d, S, chunk, ns, n_lin;
+  int* err;
+  bf16_t* out;
+  ProjArgs proj;  // QG: the query projection
+};
+
+__device__ __forceinline__ void row_issue(const bf16_t* base, int k0, int k1, int slot, int sub, u32x4 (&r)[8]) {
+  __builtin_amdgcn_sched_barrier(0);  // issue exactly here: the schedule is the point (the compiler would sink these
+#pragma unroll                        // loads below the next chunk's arithmetic and wait on them there)
+  for (int j = 0; j < 8; ++j) r[j] = ld_row8<bf16_t>(base + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8).u[0];
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// one chunk of the pair: its scores from K (then the caller's next V load goes out, the K registers being dead),
+// its values from V, merged into the wave's running (M, Lr, A)
+__device__ __forceinline__ void row_fold(float mw, const float (&sc)[8], const u32x4 (&vr)[8], int k0, int k1, int slot,
+                                         float& M, float& Lr, float (&A)[8]) {
+  float lw, acc[8], f0 = 0.f, f1 = 0.f;
+  wave_values_bf16(sc, mw, vr, k0, k1, slot, 8, lw, acc);
+  const int mode = fold_begin(mw, lw, M, Lr, f0, f1);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) A[i] = fold_value(mode, A[i], acc[i], f0, f1);
+}
+
+template <bool QG, int NS>  // NS chunks per pair (6 for Whisper's 1500 frames): a static schedule, static load counts
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void cross_attn_row_kernel(CRP p) {
+  __shared__ __attribute__((aligned(16))) char scratch[QG ? PROJ_SCRATCH : 16];
+  __shared__ float red[4][64];
+  __shared__ float stat[8];
+  if constexpr (QG) {
+    if ((int)blockIdx.x < p.n_lin) {
+      proj_publish_granules(p.proj, blockIdx.x, scratch, p.qg);
+      return;
+    }
+  }
+  const int row = blockIdx.x - (QG ? p.n_lin : 0);
+  const int h = row % p.H, b = row / p.H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
+  const bf16_t* kb = p.kc + ((int64_t)b * p.H + h) * p.S * HD;
+  const bf16_t* vb = p.vc + ((int64_t)b * p.H + h) * p.S * HD;
+  unsigned long long* qg = QG ? p.qg + (int64_t)b * (p.d / 2) + h * 32 : nullptr;
+  // the query's loads first, then the first two chunks' K / V
+  unsigned long long g[4];
+  u32x4 qraw;
+  if constexpr (QG) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) g[i] = peek_granule(qg + sub * 4 + i);
+  } else {
+    qraw = *reinterpret_cast<const u32x4*>(p.q + (int64_t)b * p.d + h * HD + sub * 8);
+  }
+  constexpr int ns = NS;
+  const int chunk = p.chunk, S = p.S;
+  // three 32-register K / V sets in rotation: chunk c + 1's K goes out before chunk c's scores, its V right
+  // after them (into chunk c's dead K registers), chunk c + 2's K after chunk c's values (into its dead V
+  // registers) -- one chunk in flight while one is computed, 96 K / V registers live
+  u32x4 r0[8], r1[8], r2[8];
+  row_issue(kb, 0, min(S, chunk), slot, sub, r0);
+  row_issue(vb, 0, min(S, chunk), slot, sub, r1);
+  if (ns > 1) row_issue(kb, chunk, min(S, 2 * chunk), slot, sub, r2);
+  if constexpr (QG) {
+    bool ok = ((g[0] & g[1] & g[2] & g[3]) >> 32) == 1ull;
+    for (int it = 0; __builtin_amdgcn_ballot_w64(!ok) != 0; ++it) {  // the projection not yet published: poll
+      if (it >= XG_SPIN_LIMIT) {
+        if (!ok) {
+          __hip_atomic_store(p.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) g[i] = 0x7fc07fc0ull | (1ull << 32);  // bf16 NaN pairs: the row fails loudly
+          ok = true;
+        }
+        continue;
+      }
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) g[i] = peek_granule(qg + sub * 4 + i);
+      ok = ((g[0] & g[1] & g[2] & g[3]) >> 32) == 1ull;
+    }
+    qraw = u32x4{(uint32_t)g[0], (uint32_t)g[1], (uint32_t)g[2], (uint32_t)g[3]};
+  }
+  float ql[8];
+  {
+    Row8<bf16_t> qr;
+    qr.u[0] = qraw;
+    unpack8<bf16_t>(qr, ql);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ql[i] *= LOG2E;
+  }
+  float M = -INFINITY, Lr = 0.f, A[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) A[i] = 0.f;
+  // chunk c: K in rk, V in rv (the next chunk's K already in the third set); after the step V(c + 1) is in rk
+  // and K(c + 2) in rv
+  auto step = [&](const int c, u32x4 (&rk)[8], u32x4 (&rv)[8]) __attribute__((always_inline)) {
+    float sc[8];
+    const int k0 = c * chunk, k1 = min(S, k0 + chunk);
+    const float mw = wave_scores_bf16(ql, rk, k0, k1, slot, 8, sc);
+    if (c + 1 < ns) row_issue(vb, k1, min(S, k1 + chunk), slot, sub, rk);
+    row_fold(mw, sc, rv, k0, k1, slot, M, Lr, A);
+    if (c + 2 < ns) row_issue(kb, k0 + 2 * chunk, min(S, k0 + 3 * chunk), slot, sub, rv);
+  };
+#pragma unroll
+  for (int c = 0; c < ns; c += 3) {
+    step(c, r0, r1);                      // K(c) r0, V(c) r1 -> V(c+1) r0, K(c+2) r1
+    if (c + 1 < ns) step(c + 1, r2, r0);  // K(c+1) r2, V(c+1) r0 -> V(c+2) r2, K(c+3) r0
+    if (c + 2 < ns) step(c + 2, r1, r2);  // K(c+2) r1, V(c+2) r2 -> V(c+3) r1, K(c+4) r2
+  }
   if (lane < 8) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
+    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = A[i];
   }
   if (lane == 0) {
-    stat[wave] = mw;
-    stat[4 + wave] = lw;
+    stat[wave] = M;
+    stat[4 + wave] = Lr;
   }
   __syncthreads();
   float m, l, o;
   merge_waves_bf16(stat, red, tid, m, l, o);
-  bf16_t* orow = p.out + (int64_t)b * p.d + h * HD;
-  if (ns == 1) {
-    if (tid < HD) TypeIO<bf16_t>::st(orow + tid, o / l);
-  } else {
-    publish_granules_and_combine<bf16_t>(p.gran + (int64_t)row * ns * (HD + 2), ns, split, m, l, o, orow, p.err);
+  if (tid < HD) TypeIO<bf16_t>::st(p.out + (int64_t)b * p.d + h * HD + tid, o / l);
+  if constexpr (QG) {
+    if (tid < 32)  // re-arm the row's query for the next launch (every wave of this, its only reader, has read it)
+      __hip_atomic_store(qg + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (split == ns - 1 && tid < 32)  // re-arm the row's query for the next launch (every chunk has read it)
-    __hip_atomic_store(qg + tid, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Cross-attention for several query rows of one item (the prefill's P prompt positions, and the beams of
@@ -1332,10 +1485,17 @@ extern "C" int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, in
   if (!qkv || !out || B <= 0 || H <= 0 || T <= 0) return kw_set_error_msg(KW_EINVAL, "kw_attention: invalid arguments");
   if (hd != HD) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_attention: head_dim must be 64");
   hipStream_t s = (hipStream_t)stream;
+  const bool ql2 = (dtype & KW_ATTN_Q_LOG2) != 0;
+  dtype &= ~KW_ATTN_Q_LOG2;
+  if (ql2 && dtype != KW_DT_BF16) return kw_set_error_msg(KW_EUNSUPPORTED, "kw_attention: KW_ATTN_Q_LOG2 is bf16 only");
   if (dtype == KW_DT_BF16) {
     const int64_t grid = B * H * ((T + AQ - 1) / AQ);
-    hipLaunchKernelGGL(attn_fwd_bf16, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)qkv, (int)B, (int)H, (int)T,
-                       (bf16_t*)out);
+    if (ql2)
+      hipLaunchKernelGGL(attn_fwd_bf16<true>, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)qkv, (int)B, (int)H,
+                         (int)T, (bf16_t*)out);
+    else
+      hipLaunchKernelGGL(attn_fwd_bf16<false>, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)qkv, (int)B, (int)H,
+                         (int)T, (bf16_t*)out);
   } else if (dtype == KW_DT_F32) {
     const int64_t grid = B * H * ((T + 3) / 4);
     hipLaunchKernelGGL(attn_fwd_f32, dim3((unsigned)grid), dim3(256), 0, s, (const float*)qkv, (int)B, (int)H, (int)T,
@@ -1392,7 +1552,8 @@ static size_t cross_partials_bytes(int64_t B, int64_t q_len, int64_t H, int64_t 
 }
 
 // workspace: f32 partials [rows][ns][HD+2] | arrival counters [rows] (publish_and_combine kernels) | error word,
-// padded to 64 B | 8-byte granules [rows][ns][HD+2] (cross_attn_dma_kernel); every region zero before first use
+// padded to 64 B | 8-byte granules [rows][ns][4 waves][HD+2] (cross_attn_dma_kernel, xq_cross_kernel); every region
+// zero before first use
 static size_t cross_granule_offset(int64_t B, int64_t q_len, int64_t H, int64_t S) {
   const size_t head = cross_partials_bytes(B, q_len, H, S) + (size_t)(B * q_len * H) * sizeof(int) + sizeof(int);
   return (head + 63) & ~(size_t)63;
@@ -1400,7 +1561,26 @@ static size_t cross_granule_offset(int64_t B, int64_t q_len, int64_t H, int64_t 
 
 extern "C" size_t kw_cross_attn_workspace(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S) {
   (void)hd;
-  return cross_granule_offset(B, q_len, H, S) + 2 * cross_partials_bytes(B, q_len, H, S);
+  return cross_granule_offset(B, q_len, H, S) + 8 * cross_partials_bytes(B, q_len, H, S);  // granules per wave
+}
+
+// cross_attn_row_kernel when one round of pair workgroups covers the device -- at least one per CU, all resident
+// at once (the occupancy query) -- and the A/B switch KW_CROSS_ROW=0 is not set (read once).
+constexpr int ROW_NS = 6;  // cross_attn_row_kernel's chunk count (S = 1500)
+
+template <bool QG>
+static bool row_kernel_fits(int64_t rows, int ns) {
+  static int ncu = 0, per_cu = 0, off = -1;
+  if (off < 0) {
+    const char* e = getenv("KW_CROSS_ROW");
+    off = (e && e[0] == '0') ? 1 : 0;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&cross_attn_row_kernel<QG, ROW_NS>), 256,
+                                                     0) != hipSuccess)
+      ncu = per_cu = 0;
+  }
+  return !off && ns == ROW_NS && ncu > 0 && rows >= ncu && rows <= (int64_t)ncu * per_cu;
 }
 
 extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64_t H, int64_t hd,
@@ -1437,6 +1617,15 @@ extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q
     const dim3 gm((unsigned)(B * ((q_len + 7) / 8) * H), (unsigned)ns);
     hipLaunchKernelGGL((cross_attn_multi_kernel<bf16_t, 8>), gm, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
+  } else if (dtype == KW_DT_BF16 && q_len == 1 && row_kernel_fits<false>(B * H, ns)) {
+    CRP p{};
+    p.q = (const bf16_t*)q;
+    p.kc = (const bf16_t*)k;
+    p.vc = (const bf16_t*)v;
+    p.H = (int)H, p.d = (int)(H * HD), p.S = (int)S, p.chunk = chunk, p.ns = ns, p.n_lin = 0;
+    p.err = cnt + B * q_len * H;
+    p.out = (bf16_t*)out;
+    hipLaunchKernelGGL((cross_attn_row_kernel<false, ROW_NS>), dim3((unsigned)(B * H)), dim3(256), 0, s, p);
   } else if (dtype == KW_DT_BF16 && XA_DMA && chunk > 224 && chunk <= 256 && S - (int64_t)(ns - 1) * chunk > 224)
     hipLaunchKernelGGL(cross_attn_dma_kernel, grid, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk,
@@ -1502,6 +1691,20 @@ extern "C" int kw_dec_xq_cross(const kw_dec_xq_cross_args* a, kw_stream_t stream
   p.gran = reinterpret_cast<unsigned long long*>(ws + cross_granule_offset(a->M, 1, a->H, a->S));
   p.err = reinterpret_cast<int*>(ws + cross_partials_bytes(a->M, 1, a->H, a->S)) + a->M * a->H;
   p.out = reinterpret_cast<bf16_t*>(a->out);
+  if (row_kernel_fits<true>(a->M * a->H, p.ns)) {  // one pair workgroup per (row, head), chunks pipelined
+    CRP r{};
+    r.qg = p.qg;
+    r.kc = p.kc;
+    r.vc = p.vc;
+    r.H = p.H, r.d = p.d, r.S = p.S, r.chunk = p.chunk, r.ns = p.ns, r.n_lin = p.n_lin;
+    r.err = p.err;
+    r.out = p.out;
+    r.proj = ProjArgs{p.x, p.ldx, p.M, p.d, p.d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, p.d};
+    hipLaunchKernelGGL((cross_attn_row_kernel<true, ROW_NS>), dim3((unsigned)(p.n_lin + a->M * a->H)), dim3(256), 0,
+                       (hipStream_t)stream, r);
+    KW_CHECK_LAUNCH();
+    return KW_OK;
+  }
   const int64_t grid = p.n_lin + a->M * a->H * p.ns;
   hipLaunchKernelGGL(xq_cross_kernel, dim3((unsigned)grid), dim3(256), 0, (hipStream_t)stream, p);
   KW_CHECK_LAUNCH();

@@ -45,10 +45,11 @@ __device__ __forceinline__ void unpack8(const Row8<T>& r, float v[8]) {
 // value dims of this lane reduced over the wave's key slots.  The workgroup merges its waves' (m_w, l_w, o_w)
 // once at the end (merge_waves_bf16), and chunks merge with exp2 of log2-unit maxima.  Every multiply-add is
 // an explicit fmaf so every kernel that uses these helpers rounds identically (bitwise-equal rows).
+// the two halves of wave_row_bf16, for kernels that interleave loads between them: the scores (log2 units)
+// and the wave maximum ...
 template <int KS = 32>  // key of (slot, j) = k0 + slot + KS * j (32 key slots per 4-wave row, 16 per 2-wave row)
-__device__ __forceinline__ void wave_row_bf16(const float ql[8], const u32x4 kr[8], const u32x4 vr[8], int k0, int k1,
-                                              int slot, int nj, float& mw, float& lw, float acc[8]) {
-  float sc[8];
+__device__ __forceinline__ float wave_scores_bf16(const float ql[8], const u32x4 kr[8], int k0, int k1, int slot,
+                                                  int nj, float sc[8]) {
   float mx = -INFINITY;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -66,7 +67,13 @@ __device__ __forceinline__ void wave_row_bf16(const float ql[8], const u32x4 kr[
       mx = fmaxf(mx, sc[j]);
     }
   }
-  mx = wave_max(mx);
+  return wave_max(mx);
+}
+
+// ... then p = exp2(s - m_w), the row sum and this lane's 8 value dims reduced over the wave's key slots
+template <int KS = 32>
+__device__ __forceinline__ void wave_values_bf16(const float sc[8], float mx, const u32x4 vr[8], int k0, int k1,
+                                                 int slot, int nj, float& lw, float acc[8]) {
   float lsum = 0.f;
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = 0.f;
@@ -85,8 +92,38 @@ __device__ __forceinline__ void wave_row_bf16(const float ql[8], const u32x4 kr[
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) acc[i] = kw_sum_hi(acc[i]);
-  mw = mx;
   lw = wave_sum_dpp(lsum) * 0.125f;  // every row's p was counted by its 8 lanes (exact: power of two)
+}
+
+template <int KS = 32>
+__device__ __forceinline__ void wave_row_bf16(const float ql[8], const u32x4 kr[8], const u32x4 vr[8], int k0, int k1,
+                                              int slot, int nj, float& mw, float& lw, float acc[8]) {
+  float sc[8];
+  mw = wave_scores_bf16<KS>(ql, kr, k0, k1, slot, nj, sc);
+  wave_values_bf16<KS>(sc, mw, vr, k0, k1, slot, nj, lw, acc);
+}
+
+// One wave's running softmax over a pair's chunks, in chunk order: (M, Lr, A) absorbs the chunk's (m_w, l_w,
+// acc) -- a wave with no valid key in the chunk (m_w = -inf) is skipped, the first valid chunk is copied, later
+// ones merge with exp2 rescales.  fold_begin updates (M, Lr) and returns the mode; fold_value applies it to one
+// accumulator.  Shared by cross_attn_row_kernel (a wave folds as it streams) and the chunk-grid kernels' combine
+// (the final chunk folds every chunk's published wave partials), so the two are bitwise equal.
+__device__ __forceinline__ int fold_begin(float mw, float lw, float& M, float& Lr, float& f0, float& f1) {
+  if (mw == -INFINITY) return 0;
+  if (M == -INFINITY) {
+    M = mw;
+    Lr = lw;
+    return 1;
+  }
+  const float mn = fmaxf(M, mw);
+  f0 = __builtin_amdgcn_exp2f(M - mn);
+  f1 = __builtin_amdgcn_exp2f(mw - mn);
+  Lr = fmaf(Lr, f0, lw * f1);
+  M = mn;
+  return 2;
+}
+__device__ __forceinline__ float fold_value(int mode, float A, float acc, float f0, float f1) {
+  return mode == 0 ? A : mode == 1 ? acc : fmaf(A, f0, acc * f1);
 }
 
 // a workgroup's 4 waves: (m_w, l_w) at st[w], st[4 + w]; o_w at rd[w][dim] -> the chunk's (m, l, o[dim])

@@ -50,17 +50,31 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  // both virtual waves' weights in flight at once (HBM: the long round trip); the activation fragments (L2) of
+  // the second are loaded after the first's MFMAs (registers)
+  bf16x8 wv[2][PROJ_KTM];
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int v = min(wave + 4 * r, nv - 1);
+    const int kt0 = (nkt * v) / nv, kt1 = (nkt * (v + 1)) / nv;
+    const int ktl = max(kt1 - 1, kt0);
+    if (wave + 4 * r < nv) {
+#pragma unroll
+      for (int u = 0; u < PROJ_KTM; ++u)
+        wv[r][u] = __builtin_nontemporal_load(a.W + ((int64_t)cg * nkt + min(kt0 + u, ktl)) * 64 + lane);
+    }
+  }
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int v = wave + 4 * r;
     if (v >= nv) break;
     const int kt0 = (nkt * v) / nv, kt1 = (nkt * (v + 1)) / nv;
     const int ktl = max(kt1 - 1, kt0);
-    bf16x8 w[PROJ_KTM], a0[PROJ_KTM], a1[PROJ_KTM];
+    const bf16x8* w = wv[r];
+    bf16x8 a0[PROJ_KTM], a1[PROJ_KTM];
 #pragma unroll
     for (int u = 0; u < PROJ_KTM; ++u) {
       const int kt = min(kt0 + u, ktl);
-      w[u] = __builtin_nontemporal_load(a.W + ((int64_t)cg * nkt + kt) * 64 + lane);
       a0[u] = *reinterpret_cast<const bf16x8*>(x0 + kt * 32);
       a1[u] = *reinterpret_cast<const bf16x8*>(x1 + kt * 32);
     }

@@ -186,11 +186,11 @@ void layernorm(Tensor& x, const Tensor& gamma, const Tensor& beta, double eps, T
 }
 
 // ---- attention ----------------------------------------------------------------------------------------
-void attention(const Tensor& qkv, int64_t B, int64_t H, int64_t T, int64_t hd, Tensor& out) {
+void attention(const Tensor& qkv, int64_t B, int64_t H, int64_t T, int64_t hd, Tensor& out, int64_t flags) {
   dev(qkv, "kw_attention");
   dev(out, "kw_attention");
   c10::DeviceGuard g(qkv.device());
-  check(kw_attention(dt_of(qkv), ptr(qkv), B, H, T, hd, ptr(out), stream_of(qkv)), "kw_attention");
+  check(kw_attention(dt_of(qkv) | (int)flags, ptr(qkv), B, H, T, hd, ptr(out), stream_of(qkv)), "kw_attention");
 }
 
 void embed(const Tensor& ids, int64_t B, int64_t q_len, const Tensor& cur_len, const Tensor& tok_emb,
@@ -419,7 +419,7 @@ TORCH_LIBRARY(kw, m) {
         "Tensor(c!)? hb, Tensor(d!) workspace, int[] geo, float ln_eps, float scale) -> ()");
   m.def("pack_weight(Tensor W, Tensor(a!) out) -> ()");
   m.def("layernorm(Tensor(a!) x, Tensor gamma, Tensor beta, float eps, Tensor(b!) y, Tensor? delta) -> ()");
-  m.def("attention(Tensor qkv, int B, int H, int T, int hd, Tensor(a!) out) -> ()");
+  m.def("attention(Tensor qkv, int B, int H, int T, int hd, Tensor(a!) out, int flags=0) -> ()");
   m.def("embed(Tensor ids, int B, int q_len, Tensor cur_len, Tensor tok_emb, Tensor pos_emb, Tensor(a!) h, "
         "Tensor(b!)? hb) -> ()");
   m.def("self_attn_step(Tensor qkv, int B, int q_len, int H, int hd, Tensor(a!) k_cache, Tensor(b!) v_cache, "

@@ -204,14 +204,17 @@ class WhisperEngine:
         plans.append(ops.GemmPlan(bf.conv, self.conv2_w, bf.h, M, d, 3 * d, bias=self.conv2_b,
                                   lda=2 * d, a_rows_per_batch=T, a_batch_stride=(F + 2) * d,
                                   gelu=True, row_add=self.enc_pos, row_add_period=T))
-        scale = _HD ** -0.5
+        # bf16: q also carries log2(e) (folded into the QKV epilogue's q scale: one bf16 rounding, as before), so
+        # the attention's softmax takes its exponents straight off the matrix cores (kw_attention KW_ATTN_Q_LOG2)
+        ql2 = self.dtype == torch.bfloat16
+        scale = _HD ** -0.5 * (1.4426950408889634 if ql2 else 1.0)
         dl, pending = bf.delta, None  # pending: the delta the next LayerNorm must add into h first
         for lay in self.enc_layers:
             plans.append(("ln", bf.h, lay["ln1_g"], lay["ln1_b"], bf.x, pending))
             plans.append(ops.GemmPlan(bf.x, lay["qkv_w"], bf.qkv, M, 3 * d, d, bias=lay["qkv_b"],
                                       epilogue=L.KW_EPI_HEADSPLIT, scale=scale, scale_cols=d,
                                       hs_seq=T, hs_heads=self.H, hs_head_dim=_HD))
-            plans.append(("attn", bf.qkv, bf.attn))
+            plans.append(("attn", bf.qkv, bf.attn, ql2))
             if dl is None:
                 plans.append(ops.GemmPlan(bf.attn, lay["o_w"], bf.h, M, d, d, bias=lay["o_b"], epilogue=L.KW_EPI_RESID))
             else:
@@ -255,7 +258,7 @@ class WhisperEngine:
                 if p[0] == "ln":
                     ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4], delta=p[5])
                 else:
-                    ops.attention(p[1], B, self.H, T, _HD, p[2])
+                    ops.attention(p[1], B, self.H, T, _HD, p[2], q_log2=p[3])
             else:
                 p()
         return bf.out

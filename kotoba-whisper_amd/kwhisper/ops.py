@@ -285,14 +285,19 @@ def pack_weight(W: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def attention(qkv: torch.Tensor, B: int, H: int, T: int, hd: int, out: torch.Tensor):
+KW_ATTN_Q_LOG2 = 0x100
+
+
+def attention(qkv: torch.Tensor, B: int, H: int, T: int, hd: int, out: torch.Tensor, q_log2: bool = False):
+    """Encoder self-attention; ``q_log2``: q also carries log2(e) (bf16 only; kw_attention's KW_ATTN_Q_LOG2)."""
     _cuda(qkv, out)
     if qkv.numel() != 3 * B * H * T * hd or out.numel() != B * T * H * hd or qkv.dtype != out.dtype:
         raise ValueError("attention: qkv must hold [3][B][H][T][hd] and out [B][T][H*hd] of one dtype")
+    flags = KW_ATTN_Q_LOG2 if q_log2 else 0
     if _BACKEND == "torch":
-        _kw().attention(qkv, B, H, T, hd, out)
+        _kw().attention(qkv, B, H, T, hd, out, flags)
     else:
-        L.check(_lib().kw_attention(_dt(qkv), _p(qkv), B, H, T, hd, _p(out), _s()), "kw_attention")
+        L.check(_lib().kw_attention(_dt(qkv) | flags, _p(qkv), B, H, T, hd, _p(out), _s()), "kw_attention")
     return out
 
 

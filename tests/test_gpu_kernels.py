@@ -310,6 +310,29 @@ def test_attention_bf16_spike():
     torch.testing.assert_close(out.float(), _ref_attn(qkv, B, H, T, hd), atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("B,H,T", [(2, 3, 100), (1, 4, 1500), (3, 2, 1501)])
+def test_attention_bf16_q_log2(B, H, T):
+    """KW_ATTN_Q_LOG2: q carries log2(e) (the bf16 engine's QKV epilogue folds it into the q scale) and the
+    MFMA accumulates the scores onto -m_run, so p = exp2(s) is one v_exp per score.  Within bf16 rounding of
+    fp32 softmax(q k^T) v for the q it was given (divided back by log2 e), as the natural-unit kernel is for
+    its own, including a late dominant key (the reference moves) and a ragged last tile."""
+    hd = 64
+    qkv = (torch.randn(3, B, H, T, hd, device="cuda") * 0.5)
+    qkv[0] *= 0.125 * 8
+    qkv[1, 0, 0, T - 7] = qkv[0, 0, 0, 3] * 30  # one query's score spikes in the last tile
+    q2 = qkv.clone()
+    q2[0] *= 1.4426950408889634
+    qkv, q2 = qkv.bfloat16(), q2.bfloat16()
+    out = torch.empty(B, T, H * hd, device="cuda", dtype=torch.bfloat16)
+    ops.attention(q2, B, H, T, hd, out, q_log2=True)
+    ref_q = q2.float().clone()
+    ref_q[0] /= 1.4426950408889634
+    torch.testing.assert_close(out.float(), _ref_attn(ref_q, B, H, T, hd), atol=3e-2, rtol=2e-2)
+    nat = torch.empty_like(out)  # the natural-unit kernel on its own (differently rounded) q: the same bar
+    ops.attention(qkv, B, H, T, hd, nat)
+    torch.testing.assert_close(nat.float(), _ref_attn(qkv, B, H, T, hd), atol=3e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("B,H,T", [(2, 3, 100), (1, 6, 1500)])
 def test_attention_f32(B, H, T):
     hd = 64
@@ -390,6 +413,68 @@ def test_cross_attn_step_b32_repeated():
     _check_cross_ws_rearmed(ws, B * H, S)
 
 
+@pytest.mark.parametrize("B,H", [(32, 20), (13, 20), (44, 6)])
+def test_cross_attn_step_pair_kernel(B, H):
+    """One workgroup per (row, head) pair streaming its six 250-key chunks with the next chunk in flight
+    (cross_attn_row_kernel: B H between the CU count and what fits at once -- 640, 260 and 264 pairs here):
+    close to fp32 softmax(q K^T) V, deterministic, and it leaves the workspace untouched (zero)."""
+    S, hd = 1500, 64
+    torch.manual_seed(B * 100 + H)
+    k = torch.randn(B, H, S, hd, device="cuda").bfloat16()
+    v = torch.randn(B, H, S, hd, device="cuda").bfloat16()
+    q = (torch.randn(B, H * hd, device="cuda") * 0.3).bfloat16()
+    out = torch.empty(B, H * hd, device="cuda", dtype=torch.bfloat16)
+    ws = torch.zeros(ops.cross_attn_workspace_bytes(B, 1, H, hd, S) // 4 + 1, device="cuda")
+    ops.cross_attn_step(q, B, 1, H, hd, k, v, S, out, ws)
+    first = out.clone()
+    for _ in range(3):
+        ops.cross_attn_step(q, B, 1, H, hd, k, v, S, out, ws)
+        assert torch.equal(out, first)
+    qq = q.float().view(B, 1, H, hd).permute(0, 2, 1, 3)
+    ref = (torch.softmax(qq @ k.float().transpose(-1, -2), -1) @ v.float()).permute(0, 2, 1, 3).reshape(B, H * hd)
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+    assert int(ws.view(torch.int32).abs().sum()) == 0
+
+
+def test_cross_attn_batch_invariant():
+    """A greedy row's cross-attention is bitwise the same whichever grid its batch size selects: B = 32 (640
+    pairs: cross_attn_row_kernel, a wave folding its chunks as it streams) == the same rows in batches of 2
+    (40 pairs: cross_attn_dma_kernel, per-wave chunk partials folded by the last chunk) -- also through the fused
+    query projection (kw_dec_xq_cross: cross_attn_row_kernel<QG> vs xq_cross_kernel)."""
+    B, H, S, hd = 32, 20, 1500, 64
+    d = H * hd
+    torch.manual_seed(11)
+    k = torch.randn(B, H, S, hd, device="cuda").bfloat16()
+    v = torch.randn(B, H, S, hd, device="cuda").bfloat16()
+    q = (torch.randn(B, d, device="cuda") * 0.3).bfloat16()
+    big = torch.empty(B, d, device="cuda", dtype=torch.bfloat16)
+    ops.cross_attn_step(q, B, 1, H, hd, k, v, S, big, torch.zeros(ops.cross_attn_workspace_bytes(B, 1, H, hd, S) // 4 + 1,
+                                                                   device="cuda"))
+    ws2 = torch.zeros(ops.cross_attn_workspace_bytes(2, 1, H, hd, S) // 4 + 1, device="cuda")
+    small = torch.empty(2, d, device="cuda", dtype=torch.bfloat16)
+    for b0 in range(0, B, 2):
+        ops.cross_attn_step(q[b0:b0 + 2].contiguous(), 2, 1, H, hd, k[b0:b0 + 2].contiguous(), v[b0:b0 + 2].contiguous(),
+                            S, small, ws2)
+        assert torch.equal(small, big[b0:b0 + 2]), b0
+    _check_cross_ws_rearmed(ws2, 2 * H, S)
+    # fused query projection
+    eps = 1e-5
+    hb = torch.randn(B, d, device="cuda").bfloat16()
+    W = (torch.randn(d, d, device="cuda") / d ** 0.5).bfloat16()
+    packed, colsum = ops.pack_weight(W), ops.ln_colsum(W)
+    bias = torch.randn(d, device="cuda") * 0.1
+    fb = torch.empty(B, d, device="cuda", dtype=torch.bfloat16)
+    ops.XqCrossPlan(hb, packed, B, d, H, ln=(eps, colsum), bias=bias, scale=0.125, k=k, v=v, S=S, out=fb,
+                    workspace=torch.zeros(ops.xq_cross_workspace_bytes(B, d, H, S) // 4 + 1, device="cuda"))()
+    wsx = torch.zeros(ops.xq_cross_workspace_bytes(2, d, H, S) // 4 + 1, device="cuda")
+    for b0 in range(0, B, 2):
+        ops.XqCrossPlan(hb[b0:b0 + 2].contiguous(), packed, 2, d, H, ln=(eps, colsum), bias=bias, scale=0.125,
+                        k=k[b0:b0 + 2].contiguous(), v=v[b0:b0 + 2].contiguous(), S=S, out=small, workspace=wsx)()
+        assert torch.equal(small, fb[b0:b0 + 2]), b0
+    torch.cuda.synchronize()
+    assert int(wsx.view(torch.int32).abs().sum()) == 0
+
+
 def _check_cross_ws_rearmed(ws, rows, S):
     """Every launch leaves the workspace as it needs the next one: arrival counters 0, the error word 0 (no
     granule poll timed out), every {value, tag} granule re-armed to 0 by its combining split."""
@@ -398,16 +483,18 @@ def _check_cross_ws_rearmed(ws, rows, S):
     w = ws.view(torch.int32)
     assert int(w[part: part + rows].abs().sum()) == 0, "arrival counters not reset"
     assert int(w[part + rows]) == 0, "cross-attention granule poll timed out"
-    g0 = (4 * (part + rows + 1) + 63) // 64 * 16  # granule region, in int32 words
-    assert int(w[g0: g0 + 2 * part].abs().sum()) == 0, "granules not re-armed"
+    g0 = (4 * (part + rows + 1) + 63) // 64 * 16  # granule region [rows][ns][4 waves][66] x 8 B, in int32 words
+    assert int(w[g0: g0 + 8 * part].abs().sum()) == 0, "granules not re-armed"
 
 
 @pytest.mark.parametrize("q_len", [2, 3, 4, 5, 8, 13, 20, 32, 45])
 @pytest.mark.parametrize("S", [1500, 200])
 def test_cross_attn_multirow_bitwise(q_len, S):
-    """bf16 rows of one item sharing a K/V pass (prefill positions, beams) == each row attended alone by
-    the one-row kernel: bit for bit up to 4 rows (the same f32 arithmetic per row); from 5 rows the matrix-
-    core kernel takes P in bf16, within bf16 rounding (atol 1e-2, rtol 1e-2)."""
+    """bf16 rows of one item sharing a K/V pass (prefill positions, beams) vs each row attended alone by
+    the one-row kernel: up to 4 rows the same f32 arithmetic per chunk -- bit for bit with one chunk (S = 200);
+    over several chunks the one-row kernels fold per-wave chunk partials (bitwise cross_attn_row_kernel's,
+    so greedy rows are batch-invariant) while the multi-row kernel merges per chunk, within f32 reassociation
+    (atol 2e-3); from 5 rows the matrix-core kernel takes P in bf16, within bf16 rounding (atol 1e-2)."""
     B, H, hd = 3, 20, 64
     d = H * hd
     dtype = torch.bfloat16
@@ -423,8 +510,10 @@ def test_cross_attn_multirow_bitwise(q_len, S):
     qv = q.view(B, q_len, d)
     for i in range(q_len):
         ops.cross_attn_step(qv[:, i].contiguous(), B, 1, H, hd, k, v, S, one, ws1)
-        if q_len <= 4:
+        if q_len <= 4 and S <= 256:
             assert torch.equal(out.view(B, q_len, d)[:, i], one), i
+        elif q_len <= 4:
+            torch.testing.assert_close(out.view(B, q_len, d)[:, i].float(), one.float(), atol=2e-3, rtol=1e-2)
         else:
             torch.testing.assert_close(out.view(B, q_len, d)[:, i].float(), one.float(), atol=1e-2, rtol=1e-2)
     _check_cross_ws_rearmed(ws1, B * H, S)
@@ -771,7 +860,7 @@ def test_qkv_self_fused_matches_two_launches(M, d, H, L):
 
 # ---------------------------------------------------------------- fused cross-attention query + step
 @pytest.mark.parametrize("M,d,H,S", [(32, 1280, 20, 1500), (7, 1280, 20, 1500), (1, 384, 6, 1500),
-                                     (32, 384, 6, 500), (5, 512, 8, 240)])
+                                     (32, 384, 6, 500), (5, 512, 8, 240), (32, 512, 8, 1500)])
 def test_xq_cross_fused_matches_two_launches(M, d, H, S):
     """kw_dec_xq_cross == kw_dec_linear(xq, LayerNorm fused, every column scaled) then kw_cross_attn_step(q_len 1),
     bit for bit (the projection is dec_linear's arithmetic on virtual waves, the attention cross_attn_dma_kernel's),
