@@ -314,12 +314,18 @@ def main(argv=None):
             for pl in xc_plans:
                 pl()
 
-        cross_kernel = "xq_cross_kernel"
         d_model = shape.d_model
         # K + V of one layer (bf16) + the query projection's weights and activation rows, per launch
         cross_bytes = 2 * B * H * S * hd * 2 + d_model * d_model * 2 + B * d_model * 2
-        cross_note = ("xq_cross_kernel (decoder cross-attention: LayerNorm-fused query projection + the K/V stream "
-                      "in one launch, K by LDS-DMA; one launch per layer; rocprof name)")
+        if ops.cross_attn_pair_kernel(B * H, S, fused=True):
+            cross_kernel = "cross_attn_row_kernel<true"
+            cross_note = ("cross_attn_row_kernel<true, 6> (kw_dec_xq_cross: the LayerNorm-fused query projection's "
+                          "workgroups, then one workgroup per (row, head) pair streaming its six K/V chunks with the "
+                          "next in flight; one launch per layer; rocprof name)")
+        else:
+            cross_kernel = "xq_cross_kernel"
+            cross_note = ("xq_cross_kernel (kw_dec_xq_cross: LayerNorm-fused query projection + one workgroup per "
+                          "(row, head, chunk), K by LDS-DMA; one launch per layer; rocprof name)")
     else:
         def cross_all_layers():  # one launch per layer, each on its own K/V: no Infinity-Cache reuse
             for li in range(n_dec):

@@ -228,6 +228,12 @@ int kw_dec_xq_cross(const kw_dec_xq_cross_args* args, kw_stream_t stream);
 size_t kw_dec_xq_cross_workspace(int64_t M, int64_t d, int64_t H, int64_t S);
 int kw_dec_xq_cross_supported(int64_t M, int64_t d, int64_t H, int64_t S);
 
+/* Which grid a bf16 one-row cross-attention of `rows` = B * H (row, head) pairs over S keys launches (for
+ * profilers naming kernels): 1 = one workgroup per pair streaming its chunks (cross_attn_row_kernel; used when
+ * the pairs fill the CUs and fit at once and S = 1500), 0 = one workgroup per (pair, chunk).  fused: the
+ * kw_dec_xq_cross variant.  Both give bitwise the same rows. */
+int kw_cross_attn_pair_kernel(int64_t rows, int64_t S, int fused);
+
 /* Decoder cross-attention against cached encoder K/V [B][H][S][hd] (TF modeling_whisper.py:323-326).
  * q: [B*q_len][H*hd]; out: [B*q_len][H*hd]; S <= 2048; workspace >= kw_cross_attn_workspace(...) bytes and
  * ZERO-FILLED before its first use (it holds arrival counters that every call leaves at zero). */

@@ -570,21 +570,18 @@ __device__ __forceinline__ void wave_partials_combine(unsigned long long* gr, in
                                                       bf16_t* out_row, int* err) {
   constexpr int G = HD + 2, NSMAX = 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (split != ns - 1) {
-    unsigned long long* w = gr + ((int64_t)split * 4 + wave) * G;
-    if (lane < 8) {
+  if (lane < 8) {  // the wave's partial of dim d = lane*8 + i, read back by lane d of the same wave (in order)
 #pragma unroll
-      for (int i = 0; i < 8; ++i) put_granule(w + 2 + lane * 8 + i, acc[i]);
-    }
+    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
+  }
+  if (split != ns - 1) {  // one contiguous 512-B granule store per wave (whole lines: no partial write-through)
+    unsigned long long* w = gr + ((int64_t)split * 4 + wave) * G;
+    put_granule(w + 2 + lane, red[wave][lane]);
     if (lane == 0) {
       put_granule(w, mw);
       put_granule(w + 1, lw);
     }
     return;
-  }
-  if (lane < 8) {  // this chunk's own partial of dim d = lane*8 + i, read back by lane d of the same wave
-#pragma unroll
-    for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
   }
   // lane d of wave w: every earlier chunk's (m, l, acc[d]) of wave w in flight at once (indices clamped: the
   // loads are unconditional, one round trip), then one check
@@ -1581,6 +1578,11 @@ static bool row_kernel_fits(int64_t rows, int ns) {
       ncu = per_cu = 0;
   }
   return !off && ns == ROW_NS && ncu > 0 && rows >= ncu && rows <= (int64_t)ncu * per_cu;
+}
+
+extern "C" int kw_cross_attn_pair_kernel(int64_t rows, int64_t S, int fused) {
+  const int ns = cross_splits(S);
+  return (fused ? row_kernel_fits<true>(rows, ns) : row_kernel_fits<false>(rows, ns)) ? 1 : 0;
 }
 
 extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64_t H, int64_t hd,

@@ -385,6 +385,12 @@ def xq_cross_supported(M, d, H, S) -> bool:
     return bool(_lib().kw_dec_xq_cross_supported(int(M), int(d), int(H), int(S)))
 
 
+def cross_attn_pair_kernel(rows, S, fused=False) -> bool:
+    """Whether a bf16 one-row cross-attention of ``rows`` (row, head) pairs runs as one workgroup per pair
+    (cross_attn_row_kernel) rather than per (pair, chunk) -- kernel naming for profiles; results are equal."""
+    return bool(_lib().kw_cross_attn_pair_kernel(int(rows), int(S), int(bool(fused))))
+
+
 class XqCrossPlan:
     """A pre-built ``kw_dec_xq_cross`` call: the LayerNorm-fused cross-attention query projection and the
     cross-attention step (q_len 1) in one launch (bitwise kw_dec_linear(xq) then kw_cross_attn_step).  ``x``: hb [M][ldx] bf16; ``W`` packed (gamma folded), ``ln`` = (eps, colsum [d]), ``bias``

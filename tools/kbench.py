@@ -102,8 +102,8 @@ def main():
             plans.append(ops.DecLinearPlan(hb, W, B, N, K, **kw))
         us = timeit(plans, a.reps)
         res[name] = {"us": round(us, 2), "GBps": round(N * K * 2 / us / 1e3, 1)}
-    # attention kernels
-    if not want("cross_attn") and not want("self_attn"):
+    # attention kernels (and the fused decode blocks: kw_dec_xq_cross, kw_dec_qkv_self)
+    if not any(want(n) for n in ("cross_attn", "xq_cross", "self_attn", "qkv_self")):
         print(json.dumps(res))
         return
     q = torch.randn(B, d, device=dev).bfloat16()
@@ -115,7 +115,17 @@ def main():
         us = timeit(fns, max(1, a.reps // 4))
         res["cross_attn"] = {"us": round(us, 2), "GBps": round(2 * B * H * S * 64 * 2 / us / 1e3, 1)}
         del cross
-    if not want("self_attn"):
+    if want("xq_cross"):  # the greedy step's cross block: LN-fused q projection + attention, per-layer K/V
+        cross = [torch.randn(2, B, H, S, 64, device=dev).bfloat16() for _ in range(nl)]
+        Wq = [ops.pack_weight((torch.randn(d, d, device=dev) / d ** 0.5).bfloat16()) for _ in range(nl)]
+        cs, bq = torch.zeros(d, device=dev), torch.zeros(d, device=dev)
+        wsx = torch.zeros(ops.xq_cross_workspace_bytes(B, d, H, S) // 4 + 1, device=dev)
+        plans = [ops.XqCrossPlan(hb, Wq[i], B, d, H, ln=(1e-5, cs), bias=bq, scale=0.125, k=cross[i][0], v=cross[i][1],
+                                 S=S, out=out, workspace=wsx, ldx=F) for i in range(nl)]
+        us = timeit(plans, max(1, a.reps // 4))
+        res["xq_cross"] = {"us": round(us, 2), "GBps": round((2 * B * H * S * 64 * 2 + d * d * 2) / us / 1e3, 1)}
+        del cross, Wq, plans
+    if not want("self_attn") and not want("qkv_self"):
         print(json.dumps(res))
         return
     kc = torch.randn(nl, B, H, 448, 64, device=dev).bfloat16()
@@ -126,7 +136,17 @@ def main():
         cur = torch.tensor([t], dtype=torch.int32, device=dev)
         fns = [lambda i=i, cur=cur: ops.self_attn_step(qkv, B, 1, H, 64, kc[i], vc[i], 448, cur, out, sws)
                for i in range(nl)]
-        res[f"self_attn_t{t}"] = {"us": round(timeit(fns, a.reps), 2)}
+        if want("self_attn"):
+            res[f"self_attn_t{t}"] = {"us": round(timeit(fns, a.reps), 2)}
+        if want("qkv_self"):  # the greedy step's self block: LN-fused qkv projection + attention + cache append
+            Wqkv = [ops.pack_weight((torch.randn(3 * d, d, device=dev) / d ** 0.5).bfloat16()) for _ in range(nl)]
+            cs3, b3 = torch.zeros(3 * d, device=dev), torch.zeros(3 * d, device=dev)
+            qws = torch.zeros(ops.qkv_self_workspace_bytes(B, d) // 4 + 1, device=dev)
+            plans = [ops.QkvSelfPlan(hb, Wqkv[i], B, d, H, ln=(1e-5, cs3), bias=b3, scale=0.125, k_cache=kc[i],
+                                     v_cache=vc[i], t_max=448, cur_len=cur, out=out, workspace=qws, ldx=F)
+                     for i in range(nl)]
+            res[f"qkv_self_t{t}"] = {"us": round(timeit(plans, a.reps), 2)}
+            del Wqkv, plans
     print(json.dumps(res))
 
 

@@ -6,7 +6,7 @@ TAG=${1:-r01}
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-ONLY=cross_attn,self_attn_t132,o_resid,fc1_ln_gelu,fc2_resid,qkv_ln,xq_ln,lm_head
+ONLY=cross_attn,xq_cross,self_attn,qkv_self,o_resid,fc1_ln_gelu,fc2_resid,qkv_ln,xq_ln,lm_head
 rm -rf gpurun_out/${TAG}_pmc_fetch gpurun_out/${TAG}_pmc_write
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/${TAG}_pmc_fetch -o run -- python3 tools/kbench.py --eager --reps 2 --only $ONLY > gpurun_out/${TAG}_pmc_fetch.log 2>&1
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/${TAG}_pmc_write -o run -- python3 tools/kbench.py --eager --reps 2 --only $ONLY > gpurun_out/${TAG}_pmc_write.log 2>&1
