@@ -120,8 +120,9 @@ def main():
         Wq = [ops.pack_weight((torch.randn(d, d, device=dev) / d ** 0.5).bfloat16()) for _ in range(nl)]
         cs, bq = torch.zeros(d, device=dev), torch.zeros(d, device=dev)
         wsx = torch.zeros(ops.xq_cross_workspace_bytes(B, d, H, S) // 4 + 1, device=dev)
-        plans = [ops.XqCrossPlan(hb, Wq[i], B, d, H, ln=(1e-5, cs), bias=bq, scale=0.125, k=cross[i][0], v=cross[i][1],
-                                 S=S, out=out, workspace=wsx, ldx=F) for i in range(nl)]
+        hbd = hb[:, :d].contiguous()  # the engine's q = 1 residual mirror: [B][d]
+        plans = [ops.XqCrossPlan(hbd, Wq[i], B, d, H, ln=(1e-5, cs), bias=bq, scale=0.125, k=cross[i][0], v=cross[i][1],
+                                 S=S, out=out, workspace=wsx) for i in range(nl)]
         us = timeit(plans, max(1, a.reps // 4))
         res["xq_cross"] = {"us": round(us, 2), "GBps": round((2 * B * H * S * 64 * 2 + d * d * 2) / us / 1e3, 1)}
         del cross, Wq, plans
@@ -142,8 +143,9 @@ def main():
             Wqkv = [ops.pack_weight((torch.randn(3 * d, d, device=dev) / d ** 0.5).bfloat16()) for _ in range(nl)]
             cs3, b3 = torch.zeros(3 * d, device=dev), torch.zeros(3 * d, device=dev)
             qws = torch.zeros(ops.qkv_self_workspace_bytes(B, d) // 4 + 1, device=dev)
-            plans = [ops.QkvSelfPlan(hb, Wqkv[i], B, d, H, ln=(1e-5, cs3), bias=b3, scale=0.125, k_cache=kc[i],
-                                     v_cache=vc[i], t_max=448, cur_len=cur, out=out, workspace=qws, ldx=F)
+            hbd = hb[:, :d].contiguous()  # the engine's q = 1 residual mirror: [B][d]
+            plans = [ops.QkvSelfPlan(hbd, Wqkv[i], B, d, H, ln=(1e-5, cs3), bias=b3, scale=0.125, k_cache=kc[i],
+                                     v_cache=vc[i], t_max=448, cur_len=cur, out=out, workspace=qws)
                      for i in range(nl)]
             res[f"qkv_self_t{t}"] = {"us": round(timeit(plans, a.reps), 2)}
             del Wqkv, plans
