@@ -848,8 +848,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void x
   __shared__ float red[4][64];
   __shared__ float stat[8];
   if ((int)blockIdx.x < p.n_lin) {
-    proj_publish_granules(ProjArgs{p.x, p.ldx, p.M, p.d, p.d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, p.d},
-                          blockIdx.x, kv, p.qg);
+    proj_publish_granules<false>(ProjArgs{p.x, p.ldx, p.M, p.d, p.d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, p.d},
+                                 blockIdx.x, kv, p.qg);
     return;
   }
   const int rows = p.M * p.H;
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   __shared__ float stat[8];
   if constexpr (QG) {
     if ((int)blockIdx.x < p.n_lin) {
-      proj_publish_granules(p.proj, blockIdx.x, scratch, p.qg);
+      proj_publish_granules<true>(p.proj, blockIdx.x, scratch, p.qg);
       return;
     }
   }

@@ -34,6 +34,10 @@ __host__ __device__ __forceinline__ bool proj_shape_ok(int64_t M, int64_t K) {
 
 // Workgroup cg's 16 columns: every wave takes part (one __syncthreads inside); wave 0 publishes
 // gran[m * (N / 2) + n / 2] for rows m < M, tag 1 in the high word.
+// ONESHOT: both virtual waves' weight AND activation fragments in flight at once (one memory round trip; 60 more
+// registers -- for kernels already at <= 3 workgroups per CU); otherwise the second virtual wave's activation
+// fragments load after the first's MFMAs.
+template <bool ONESHOT>
 __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg, char* scratch,
                                                       unsigned long long* gran) {
   f32x4(*red)[2][64] = reinterpret_cast<f32x4(*)[2][64]>(scratch);           // [8][2][64]
@@ -50,8 +54,7 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
-  // both virtual waves' weights in flight at once (HBM: the long round trip); the activation fragments (L2) of
-  // the second are loaded after the first's MFMAs (registers)
+  // both virtual waves' weights in flight at once (HBM: the long round trip)
   bf16x8 wv[2][PROJ_KTM];
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
@@ -64,20 +67,29 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
         wv[r][u] = __builtin_nontemporal_load(a.W + ((int64_t)cg * nkt + min(kt0 + u, ktl)) * 64 + lane);
     }
   }
+  bf16x8 av[2][2][PROJ_KTM];  // [round][row half][k-tile]
+  auto load_a = [&](int r) {
+    const int v = min(wave + 4 * r, nv - 1);
+    const int kt0 = (nkt * v) / nv, kt1 = (nkt * (v + 1)) / nv;
+    const int ktl = max(kt1 - 1, kt0);
+#pragma unroll
+    for (int u = 0; u < PROJ_KTM; ++u) {
+      const int kt = min(kt0 + u, ktl);
+      av[r][0][u] = *reinterpret_cast<const bf16x8*>(x0 + kt * 32);
+      av[r][1][u] = *reinterpret_cast<const bf16x8*>(x1 + kt * 32);
+    }
+  };
+  load_a(0);
+  if (ONESHOT && wave + 4 < nv) load_a(1);
 #pragma unroll
   for (int r = 0; r < 2; ++r) {
     const int v = wave + 4 * r;
     if (v >= nv) break;
     const int kt0 = (nkt * v) / nv, kt1 = (nkt * (v + 1)) / nv;
-    const int ktl = max(kt1 - 1, kt0);
     const bf16x8* w = wv[r];
-    bf16x8 a0[PROJ_KTM], a1[PROJ_KTM];
-#pragma unroll
-    for (int u = 0; u < PROJ_KTM; ++u) {
-      const int kt = min(kt0 + u, ktl);
-      a0[u] = *reinterpret_cast<const bf16x8*>(x0 + kt * 32);
-      a1[u] = *reinterpret_cast<const bf16x8*>(x1 + kt * 32);
-    }
+    if (!ONESHOT && r) load_a(1);
+    const bf16x8* a0 = av[r][0];
+    const bf16x8* a1 = av[r][1];
     f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0, s0 = c0, s1 = c0, q0 = c0, q1 = c0;
 #pragma unroll
     for (int u = 0; u < PROJ_KTM; ++u)

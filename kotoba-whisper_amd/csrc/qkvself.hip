@@ -47,14 +47,14 @@ struct QSP {
   bf16_t* out;
 };
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void qkv_self_kernel(QSP p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void qkv_self_kernel(QSP p) {
   __shared__ __attribute__((aligned(16))) char scratch[PROJ_SCRATCH];  // projection workgroups
   __shared__ float ared[QS_PAIRS][2][64];
   __shared__ float astat[QS_PAIRS][4];
   __shared__ uint32_t stage[QS_PAIRS][96];
   const int d = p.d, H = p.H, M = p.M;
   if ((int)blockIdx.x < p.n_lin) {
-    proj_publish_granules(ProjArgs{p.x, p.ldx, M, d, 3 * d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, d},
+    proj_publish_granules<true>(ProjArgs{p.x, p.ldx, M, d, 3 * d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, d},
                           blockIdx.x, scratch, p.gran);
     return;
   }
