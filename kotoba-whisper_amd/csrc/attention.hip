@@ -60,9 +60,13 @@ constexpr int TILE_BYTES = AK * HD * 2;  // 8 KB
 constexpr int ATT_LDS = 2 * 2 * TILE_BYTES;  // K,V x 2 stages = 32 KB (O staging reuses it)
 
 // QL2: q carries log2(e) too (kw_attention's KW_ATTN_Q_LOG2; the QKV GEMM epilogue folds it into the q scale,
-// one bf16 rounding as before): S^T accumulates on top of -m_run (each lane's 16 accumulators are one query's),
-// so the MFMA output is already the exponent and p = exp2(s) is ONE v_exp per score -- the softmax body's
-// per-score VALU work drops from max + fma + exp + add (+ half a cvt) to max3/2 + exp + add (+ half a cvt)
+// one bf16 rounding as before) and the matrix cores subtract the running reference: a fifth k-step per 32-key
+// block multiplies K~ = (1, 1, 0, ...) by Q~ = (hi, lo, 0, ...) with hi + lo = -m_run (two bf16 terms: exact to
+// 2^-16 of m_run), so the MFMA output is already the exponent and p = exp2(s) is ONE v_exp per score -- the
+// softmax body's per-score VALU work drops from max + fma + exp + add (+ half a cvt) to max3/2 + exp + add
+// (+ half a cvt), for one more MFMA per 16 (the alternative, accumulators initialised to -m_run, costs a
+// v_mov per score).  (Row sums as P.1 on the matrix cores too: 143 registers, 3 waves per SIMD, slower --
+// profiles/r03_lab_notes.md)
 template <bool QL2>
 __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict__ qkv, int B, int H, int T,
                                                        bf16_t* __restrict__ out) {
@@ -111,7 +115,14 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
-  float m_run = -INFINITY, l_run = 0.f;
+  float m_run = QL2 ? 0.f : -INFINITY, l_run = 0.f;
+  // QL2: the reference-subtracting fragments (lanes of k-half 0 carry the two nonzero k entries)
+  bf16x8 kone, qref;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    kone[e] = (__bf16)((hh == 0 && e < 2) ? 1.0f : 0.0f);
+    qref[e] = (__bf16)0.0f;
+  }
 
   stage(0, 0);
   for (int kt = 0; kt < n_kt; ++kt) {
@@ -123,11 +134,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
 
     // S^T for 2 key blocks of 32
     f32x16 st[2];
-    const float sinit = QL2 ? (m_run == -INFINITY ? 0.f : -m_run) : 0.f;  // (QL2: relative to the reference)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) st[i][r] = sinit;
+      for (int r = 0; r < 16; ++r) st[i][r] = 0.f;
+      if constexpr (QL2) st[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kone, qref, st[i], 0, 0, 0);  // -m_run
       const int row = i * 32 + (lane & 31);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -158,10 +169,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
     if constexpr (QL2) {
       // scores are log2-unit exponents relative to m_run (0 before the first tile); the reference moves only
       // when one exceeds it by more than 8 / ln 2 (p <= e^8 as below), then this tile is shifted once more
-      const bool bump = m_run == -INFINITY ? true : mx > 11.5415602f;
+      const bool bump = kt == 0 || mx > 11.5415602f;
       if (__builtin_amdgcn_ballot_w64(bump)) {
         const float d = bump ? mx : 0.f;  // the reference's move (a lane with no valid key keeps its reference)
-        const float alpha = (bump && m_run != -INFINITY) ? __builtin_amdgcn_exp2f(-d) : 1.0f;
+        const float alpha = (bump && kt > 0) ? __builtin_amdgcn_exp2f(-d) : 1.0f;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -170,7 +181,12 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
             st[i][r] -= d;
           }
         l_run *= alpha;
-        m_run = (m_run == -INFINITY ? 0.f : m_run) + d;
+        m_run += d;
+        const float nm = -m_run;  // the next tiles' reference as two bf16 terms
+        const __bf16 hi = (__bf16)nm;
+        const __bf16 lo = (__bf16)(nm - (float)hi);
+        qref[0] = hh == 0 ? hi : (__bf16)0.0f;
+        qref[1] = hh == 0 ? lo : (__bf16)0.0f;
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
