@@ -117,6 +117,45 @@ __global__ __launch_bounds__(256) void loop_kernel(const bf16_t* __restrict__ kc
   }
   if (x == 0x12345678u) out[blockIdx.x] = x;
 }
+
+// pair streaming (csrc/attention.hip cross_attn_row_kernel's load structure, no softmax): one workgroup per row,
+// NS chunks in order, three 8-register K / V sets in rotation (K(c+1) out before chunk c's fold, V(c+1) right
+// after the K fold, K(c+2) after the V fold)
+__device__ __forceinline__ void row_ld(const bf16_t* base, int k0, int k1, int slot, int sub, u32x4 (&r)[8]) {
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = ld_nt(base + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8);
+  __builtin_amdgcn_sched_barrier(0);
+}
+template <int NS>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void rowstream_kernel(
+    const bf16_t* __restrict__ kc, const bf16_t* __restrict__ vc, int S, int chunk, uint32_t* __restrict__ out) {
+  const int row = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, sub = lane & 7, slot = wave * 8 + (lane >> 3);
+  const bf16_t* kb = kc + (int64_t)row * S * HD;
+  const bf16_t* vb = vc + (int64_t)row * S * HD;
+  u32x4 r0[8], r1[8], r2[8];
+  row_ld(kb, 0, min(S, chunk), slot, sub, r0);
+  row_ld(vb, 0, min(S, chunk), slot, sub, r1);
+  if (NS > 1) row_ld(kb, chunk, min(S, 2 * chunk), slot, sub, r2);
+  uint32_t x = 0;
+  auto step = [&](const int c, u32x4 (&rk)[8], u32x4 (&rv)[8]) __attribute__((always_inline)) {
+    const int k0 = c * chunk, k1 = min(S, k0 + chunk);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x ^= fold(rk[j]);
+    if (c + 1 < NS) row_ld(vb, k1, min(S, k1 + chunk), slot, sub, rk);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x ^= fold(rv[j]);
+    if (c + 2 < NS) row_ld(kb, k0 + 2 * chunk, min(S, k0 + 3 * chunk), slot, sub, rv);
+  };
+#pragma unroll
+  for (int c = 0; c < NS; c += 3) {
+    step(c, r0, r1);
+    if (c + 1 < NS) step(c + 1, r2, r0);
+    if (c + 2 < NS) step(c + 2, r1, r2);
+  }
+  if (x == 0x12345678u) out[row] = x;
+}
 }  // namespace
 
 extern "C" int xa_lab_run(int variant, int per, const void* k, const void* v, int rows, int S, int ns, int nwg, void* out,
@@ -140,6 +179,10 @@ extern "C" int xa_lab_run(int variant, int per, const void* k, const void* v, in
     case 1: KW_LAB_PER(dma_kernel, grid, dim3(256), 0, s, kc, vc, S, chunk, o); break;
     case 2: KW_LAB_PER(kdma_kernel, grid, dim3(256), 0, s, kc, vc, S, chunk, o); break;
     case 3: KW_LAB_PER(loop_kernel, dim3((unsigned)nwg), dim3(256), 0, s, kc, vc, S, chunk, ns, rows * ns, o); break;
+    case 4:
+      if (ns != 6) return 5;
+      hipLaunchKernelGGL(rowstream_kernel<6>, dim3((unsigned)rows), dim3(256), 0, s, kc, vc, S, chunk, o);
+      break;
     default: return 1;
   }
   return hipGetLastError() == hipSuccess ? 0 : 4;

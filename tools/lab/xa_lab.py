@@ -53,7 +53,8 @@ def lab(variant, per, ns, nwg=0):
 q = torch.randn(B, H * HD, device=dev).bfloat16()
 o = torch.empty(B, H * HD, device=dev, dtype=torch.bfloat16)
 ws = torch.zeros(ops.cross_attn_workspace_bytes(B, 1, H, HD, S) // 4 + 1, device=dev)
-timed("production cross_attn_step", lambda li: ops.cross_attn_step(q, B, 1, H, HD, K[li], V[li], S, o, ws))
+timed("pair streaming (row kernel loads only)", lab(4, 8, 6))
+timed("production pair kernel cross_attn_step", lambda li: ops.cross_attn_step(q, B, 1, H, HD, K[li], V[li], S, o, ws))
 for ns, per in ((6, 8),):
     timed(f"reg  ns={ns} per={per}", lab(0, per, ns))
     timed(f"dma  ns={ns} per={per}", lab(1, per, ns))
@@ -64,38 +65,5 @@ if os.environ.get("XA_LAB_LOOP"):
         for occ in (2, 4, 8):
             timed(f"loop ns={ns} per={per} wg={occ}/CU", lab(3, per, ns, ncu * occ))
 
-# ---- staged copy of the production kernel (xa_lab_attn) ----
-lib.xa_lab_attn.restype = ctypes.c_int
-lib.xa_lab_attn.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                            ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-gran = torch.zeros(B * H * 6 * 66 * 2, device=dev, dtype=torch.int32)
-lo = torch.empty(B, H * HD, device=dev, dtype=torch.bfloat16)
-
-
-def attn(mode):
-    def fn(li):
-        rc = lib.xa_lab_attn(mode, q.data_ptr(), K[li].data_ptr(), V[li].data_ptr(), B, H, S, 6, gran.data_ptr(),
-                             lo.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
-        assert rc == 0, rc
-    return fn
-
-
-names = {0: "copy: production arithmetic + granules", 1: "copy: no combine", 2: "copy: fold only",
-         3: "copy: exp2 + DPP sums", 4: "copy: per-wave softmax, no mid barrier",
-         5: "copy: 4 + dot2 scores + pk_fma values"}
-ops.cross_attn_step(q, B, 1, H, HD, K[0], V[0], S, o, ws)
-ref = o.clone()
-for mode in (0, 1, 2, 3, 4, 5):
-    gran.zero_()
-    timed(names[mode], attn(mode) if mode != 1 else (lambda li, f=attn(1): (f(li), gran.zero_())))
-    if mode in (0, 3, 4, 5):
-        gran.zero_()
-        attn(mode)(0)
-        torch.cuda.synchronize()
-        err = (lo.float() - ref.float()).abs().max().item()
-        res[names[mode]]["max_err_vs_production"] = err
-        res[names[mode]]["bitwise_equal"] = bool(torch.equal(lo, ref))
-        print(f"   vs production: max err {err:.3g}, bitwise {torch.equal(lo, ref)}", flush=True)
-        gran.zero_()
 timed("production cross_attn_step (end)", lambda li: ops.cross_attn_step(q, B, 1, H, HD, K[li], V[li], S, o, ws))
 print(json.dumps(res))
