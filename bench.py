@@ -50,7 +50,7 @@ def kernel_source_files() -> list:
     with open(os.path.join(csrc, "Makefile")) as f:
         m = re.search(r"^SRCS\s*:=\s*(.+)$", f.read(), re.M)
     srcs = m.group(1).split()
-    heads = ("kw_common.h", "attn_common.h", "gemm_common.h", "processors.h")
+    heads = ("kw_common.h", "attn_common.h", "decproj.h", "gemm_common.h", "processors.h")
     return [os.path.join(csrc, x) for x in srcs + list(heads)] + [os.path.join(ROOT, "include", "kwhisper.h")]
 
 
