@@ -59,15 +59,6 @@ constexpr int AK = 64;         // keys per tile
 constexpr int TILE_BYTES = AK * HD * 2;  // 8 KB
 constexpr int ATT_LDS = 2 * 2 * TILE_BYTES;  // K,V x 2 stages = 32 KB (O staging reuses it)
 
-// QL2: q carries log2(e) too (kw_attention's KW_ATTN_Q_LOG2; the QKV GEMM epilogue folds it into the q scale,
-// one bf16 rounding as before) and the matrix cores subtract the running reference: a fifth k-step per 32-key
-// block multiplies K~ = (1, 1, 0, ...) by Q~ = (hi, lo, 0, ...) with hi + lo = -m_run (two bf16 terms: exact to
-// 2^-16 of m_run), so the MFMA output is already the exponent and p = exp2(s) is ONE v_exp per score -- the
-// softmax body's per-score VALU work drops from max + fma + exp + add (+ half a cvt) to max3/2 + exp + add
-// (+ half a cvt), for one more MFMA per 16 (the alternative, accumulators initialised to -m_run, costs a
-// v_mov per score).  (Row sums as P.1 on the matrix cores too: 143 registers, 3 waves per SIMD, slower --
-// profiles/r03_lab_notes.md)
-template <bool QL2>
 __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict__ qkv, int B, int H, int T,
                                                        bf16_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) char smem[ATT_LDS];
@@ -115,14 +106,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
-  float m_run = QL2 ? 0.f : -INFINITY, l_run = 0.f;
-  // QL2: the reference-subtracting fragments (lanes of k-half 0 carry the two nonzero k entries)
-  bf16x8 kone, qref;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    kone[e] = (__bf16)((hh == 0 && e < 2) ? 1.0f : 0.0f);
-    qref[e] = (__bf16)0.0f;
-  }
+  float m_run = -INFINITY, l_run = 0.f;
 
   stage(0, 0);
   for (int kt = 0; kt < n_kt; ++kt) {
@@ -138,7 +122,6 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) st[i][r] = 0.f;
-      if constexpr (QL2) st[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kone, qref, st[i], 0, 0, 0);  // -m_run
       const int row = i * 32 + (lane & 31);
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -166,39 +149,7 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
     mx = xor32_max(mx);
     float rs = 0.f;
     bf16x8 pf[2][2];
-    if constexpr (QL2) {
-      // scores are log2-unit exponents relative to m_run (0 before the first tile); the reference moves only
-      // when one exceeds it by more than 8 / ln 2 (p <= e^8 as below), then this tile is shifted once more
-      const bool bump = kt == 0 || mx > 11.5415602f;
-      if (__builtin_amdgcn_ballot_w64(bump)) {
-        const float d = bump ? mx : 0.f;  // the reference's move (a lane with no valid key keeps its reference)
-        const float alpha = (bump && kt > 0) ? __builtin_amdgcn_exp2f(-d) : 1.0f;
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            o[i][r] *= alpha;
-            st[i][r] -= d;
-          }
-        l_run *= alpha;
-        m_run += d;
-        const float nm = -m_run;  // the next tiles' reference as two bf16 terms
-        const __bf16 hi = (__bf16)nm;
-        const __bf16 lo = (__bf16)(nm - (float)hi);
-        qref[0] = hh == 0 ? hi : (__bf16)0.0f;
-        qref[1] = hh == 0 ? lo : (__bf16)0.0f;
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float p = __builtin_amdgcn_exp2f(st[i][8 * s + e]);  // raw v_exp_f32, arguments <= 11.5
-            rs += p;
-            pf[i][s][e] = (__bf16)p;
-          }
-    } else {
+    {
       // deferred rescale: the exponent reference m_run only moves when a score exceeds it by more than
       // 8 (p <= e^8, exact in f32 and in bf16's range); most tiles skip the O / l rescale entirely
       const bool bump = mx > m_run + 8.0f;
@@ -278,6 +229,274 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_bf16(const bf16_t* __restrict
     }
   __syncthreads();
   // each wave writes its 32 rows x 128 B: 256 16-B chunks, 4 per lane
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int chunk = i * 64 + lane;
+    const int qr = chunk >> 3, cc = chunk & 7;
+    const int q = qt * AQ + wave * 32 + qr;
+    if (q < T) {
+      const uint4 v = *reinterpret_cast<const uint4*>(os + qr * HD + cc * 8);
+      *reinterpret_cast<uint4*>(out + ((int64_t)b * T + q) * (H * HD) + h * HD + cc * 8) = v;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Encoder attention with log2-unit q (the bf16 engine, kw_attention's KW_ATTN_Q_LOG2).  q carries log2(e) too
+// (folded into the QKV GEMM epilogue's q scale: one bf16 rounding as before) and the matrix cores subtract the
+// running reference: a fifth k-step per 32-key block multiplies K~ = (1, 1, 0, ...) by Q~ = (hi, lo, 0, ...) with
+// hi + lo = -m_run (two bf16 terms: exact to 2^-16 of m_run), so the MFMA output is already the exponent and
+// p = exp2(s) is ONE v_exp per score.  The reference moves only when a score exceeds it by more than 8 / ln 2
+// (p <= e^8), then that tile is shifted once more and O / l rescaled.  The kernel is vector-issue-bound (18 MFMAs
+// per 64-key tile beside 32 v_exp, the row sums and the bf16 packing), so the tile does nothing else:
+//  * no row maximum on the common path: the tile's p = exp2(s) and row sums are computed straight away; only a
+//    wave in which some lane's sum exceeds 2980 (< e^8 = 2^11.5415602: a lane whose maximum would move the
+//    reference has a p, hence a sum, above it; NaN takes the branch too) computes the maxima, moves the
+//    reference and recomputes the tile (its scores again from the same LDS image: bitwise) -- every lane ends
+//    with the p of the always-compute-the-maximum order (r03x: bitwise equal to that kernel on every shape
+//    tested, 405 vs 460 us per launch at large-v3 B = 32, tools/lab/enc_attn_l2_ab.py);
+//  * the two ring stages as static parities (the loop unrolled by two): every LDS fragment read is a lane base
+//    plus an immediate offset;
+//  * K / V tiles by buffer_load ... lds from per-head buffer descriptors (base and size in SGPRs, advanced per
+//    tile on the scalar unit): no per-tile address arithmetic, and rows past T read as zeros (the ragged last
+//    tile's scores there are masked to -inf; their V rows enter as 0 * 0).
+// (Row sums as P.1 on the matrix cores: 143 registers, 3 waves per SIMD, slower -- profiles/r03_lab_notes.md)
+template <int N_, int PAR>  // one 16-key step of the P.V product: V^T fragments by transposed reads at immediates
+__device__ __forceinline__ void attn_vread(uint32_t b0, uint32_t b1, v2u32 (&t)[2][2]) {
+  constexpr int i = N_ >> 1, s = N_ & 1;
+  constexpr int o0 = PAR * 2 * TILE_BYTES + TILE_BYTES + (i * 32 + 16 * s) * 128;
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t[0][0]) : "v"(b0), "i"(o0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t[0][1]) : "v"(b0), "i"(o0 + 8 * 128));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t[1][0]) : "v"(b1), "i"(o0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(t[1][1]) : "v"(b1), "i"(o0 + 8 * 128));
+}
+
+__global__ __launch_bounds__(256, 4) void attn_fwd_l2(const bf16_t* __restrict__ qkv, int B, int H, int T,
+                                                      bf16_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) char smem[ATT_LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n_qt = (T + AQ - 1) / AQ;
+  const int bh = blockIdx.x / n_qt;
+  const int qt = blockIdx.x - bh * n_qt;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const int64_t head_elems = (int64_t)T * HD;
+  const bf16_t* Q = qkv + ((int64_t)(0 * B + b) * H + h) * head_elems;
+  const bf16_t* K = qkv + ((int64_t)(1 * B + b) * H + h) * head_elems;
+  const bf16_t* V = qkv + ((int64_t)(2 * B + b) * H + h) * head_elems;
+
+  const int q_lane = qt * AQ + wave * 32 + (lane & 31);
+  const int hh = lane >> 5;
+  bf16x8 qf[4];
+  {
+    const int qr = min(q_lane, T - 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(Q + (int64_t)qr * HD + 16 * s + 8 * hh);
+  }
+
+  // staging (attn_fwd_bf16's image): wave w moves rows [16w, 16w + 16) of each tile, lane = (row, 16-B slot)
+  uint32_t voff_k[2], voff_v[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = 8 * (wave * 2 + i) + (lane >> 3);
+    const int slot = lane & 7;
+    voff_k[i] = (uint32_t)(row * HD + (slot ^ ((row >> 1) & 7)) * 8) * 2;
+    voff_v[i] = (uint32_t)(row * HD + (slot ^ (((row >> 1) & 1) << 2)) * 8) * 2;
+  }
+  const int n_kt = (T + AK - 1) / AK;
+  if (T % AK) {  // rows past T: whatever the DMA leaves there must be finite (their P is 0; 0 * NaN is not)
+#pragma unroll
+    for (int i = 0; i < ATT_LDS / (256 * 16); ++i)
+      *reinterpret_cast<uint4*>(smem + (i * 256 + tid) * 16) = make_uint4(0, 0, 0, 0);
+    __syncthreads();
+  }
+  auto stage = [&](auto par_c, int kt) __attribute__((always_inline)) {
+    constexpr int par = decltype(par_c)::value;
+    const int nrec = (T - kt * AK) * HD * 2;  // this tile's rows to the head's end: later rows read as 0
+    const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc((void*)(K + (int64_t)kt * AK * HD), (short)0, nrec, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc((void*)(V + (int64_t)kt * AK * HD), (short)0, nrec, 0x00020000);
+    char* kb = smem + par * 2 * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int g = wave * 2 + i;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, (__attribute__((address_space(3))) void*)(kb + g * 1024), 16, voff_k[i], 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, (__attribute__((address_space(3))) void*)(kb + TILE_BYTES + g * 1024), 16,
+                                               voff_v[i], 0, 0, 0);
+    }
+  };
+
+  // fragment-read lane bases: K rows (lane & 31) + 32 i, 16-B chunk (2 s + hh) ^ ((row >> 1) & 7) per k-step s;
+  // V^T by transposed reads, 16-B chunk (db ^ ((qq >> 1) & 1)) * 4 + 2 grp + (pp >> 1) (attn_fwd_bf16's vread)
+  const uint32_t sbase = lds_u32(smem);
+  uint32_t kofs[4];
+  {
+    const int r = lane & 31, r7 = (r >> 1) & 7;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) kofs[s] = (uint32_t)(r * 128 + (((2 * s + hh) ^ r7) << 4));
+  }
+  uint32_t vb0, vb1;
+  {
+    const int li = lane & 15, qq = li >> 2, pp = li & 3, grp = (lane >> 4) & 1, x = (qq >> 1) & 1;
+    const uint32_t lanepart = (uint32_t)((4 * hh + qq) * 128 + (2 * grp + (pp >> 1)) * 16 + (pp & 1) * 8);
+    vb0 = sbase + lanepart + (uint32_t)((0 ^ x) * 64);
+    vb1 = sbase + lanepart + (uint32_t)((1 ^ x) * 64);
+  }
+
+  f32x16 o[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m_run = 0.f, l_run = 0.f;
+  bf16x8 kone, qref;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    kone[e] = (__bf16)((hh == 0 && e < 2) ? 1.0f : 0.0f);
+    qref[e] = (__bf16)0.0f;
+  }
+
+  auto tile = [&](auto par_c, auto first_c, int kt) __attribute__((always_inline)) {
+    constexpr int par = decltype(par_c)::value;
+    constexpr bool first = decltype(first_c)::value;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < n_kt) stage(std::integral_constant<int, 1 - par>{}, kt + 1);
+    const char* kb = smem + par * 2 * TILE_BYTES;
+
+    // S^T for 2 key blocks of 32 (log2 units, minus the reference), keys >= T masked in the ragged last tile
+    f32x16 st[2];
+    auto scores = [&]() __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) st[i][r] = 0.f;
+        st[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kone, qref, st[i], 0, 0, 0);  // -m_run
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kb + i * 32 * 128 + kofs[s]);
+          st[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], st[i], 0, 0, 0);
+        }
+      }
+      const int key0 = kt * AK;
+      if (key0 + AK > T) {  // ragged last tile only
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int key = key0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+            if (key >= T) st[i][r] = -INFINITY;
+          }
+      }
+    };
+    scores();
+    float rs;
+    bf16x8 pf[2][2];
+    auto expsum = [&]() __attribute__((always_inline)) {
+      rs = 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float p = __builtin_amdgcn_exp2f(st[i][8 * s + e]);
+            rs += p;
+            pf[i][s][e] = (__bf16)p;
+          }
+    };
+    // the reference move: only where a score exceeds the reference by more than 8 / ln 2
+    auto rebase = [&]() __attribute__((always_inline)) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[i][r]);
+      mx = xor32_max(mx);
+      const bool bump = first || mx > 11.5415602f;
+      if (__builtin_amdgcn_ballot_w64(bump)) {
+        const float d = bump ? mx : 0.f;
+        const float alpha = (bump && !first) ? __builtin_amdgcn_exp2f(-d) : 1.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            o[i][r] *= alpha;
+            st[i][r] -= d;
+          }
+        l_run *= alpha;
+        m_run += d;
+        const float nm = -m_run;
+        const __bf16 hi = (__bf16)nm;
+        const __bf16 lo = (__bf16)(nm - (float)hi);
+        qref[0] = hh == 0 ? hi : (__bf16)0.0f;
+        qref[1] = hh == 0 ? lo : (__bf16)0.0f;
+      }
+    };
+    if constexpr (first) {
+      rebase();
+      expsum();
+    } else {
+      expsum();
+      if (__builtin_amdgcn_ballot_w64(!(rs <= 2980.0f))) {  // rare: some lane may move its reference
+        // the scores again (the same MFMAs on the same LDS image: bitwise), so st need not stay live through the
+        // common path (opaque operands: the compiler would otherwise keep the first st instead)
+        asm volatile("" : "+v"(qref), "+v"(kone)::"memory");
+        scores();
+        rebase();
+        expsum();
+      }
+    }
+    l_run += xor32_sum(rs);
+
+    // O^T += V^T P^T (attn_fwd_bf16's order): step n + 1's transposed reads issued before step n's MFMAs
+    v2u32 vt[2][2][2];
+    attn_vread<0, par>(vb0, vb1, vt[0]);
+    auto pv = [&](auto n_c) __attribute__((always_inline)) {
+      constexpr int n = decltype(n_c)::value;
+      if constexpr (n + 1 < 4) {
+        attn_vread<n + 1, par>(vb0, vb1, vt[(n + 1) & 1]);
+        asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(vt[n & 1][0][0]), "+v"(vt[n & 1][0][1]), "+v"(vt[n & 1][1][0]),
+                     "+v"(vt[n & 1][1][1]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(vt[n & 1][0][0]), "+v"(vt[n & 1][0][1]), "+v"(vt[n & 1][1][0]),
+                     "+v"(vt[n & 1][1][1]));
+      }
+#pragma unroll
+      for (int db = 0; db < 2; ++db) {
+        const v4u32 w = {vt[n & 1][db][0][0], vt[n & 1][db][0][1], vt[n & 1][db][1][0], vt[n & 1][db][1][1]};
+        o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, w), pf[n >> 1][n & 1], o[db], 0, 0, 0);
+      }
+    };
+    pv(std::integral_constant<int, 0>{});
+    pv(std::integral_constant<int, 1>{});
+    pv(std::integral_constant<int, 2>{});
+    pv(std::integral_constant<int, 3>{});
+  };
+
+  using P0 = std::integral_constant<int, 0>;
+  using P1 = std::integral_constant<int, 1>;
+  using F = std::integral_constant<bool, false>;
+  stage(P0{}, 0);
+  tile(P0{}, std::integral_constant<bool, true>{}, 0);
+  int kt = 1;
+  for (; kt + 1 < n_kt; kt += 2) {
+    tile(P1{}, F{}, kt);
+    tile(P0{}, F{}, kt + 1);
+  }
+  if (kt < n_kt) tile(P1{}, F{}, kt);
+
+  // normalise and stage O (q rows x 64 hd, bf16) through LDS for coalesced stores
+  __syncthreads();
+  bf16_t* os = reinterpret_cast<bf16_t*>(smem) + wave * 32 * HD;  // 4 KB per wave
+  const float inv_l = 1.0f / l_run;
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = db * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+      os[(lane & 31) * HD + d] = f2bf(o[db][r] * inv_l);
+    }
+  __syncthreads();
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int chunk = i * 64 + lane;
@@ -1504,11 +1723,11 @@ extern "C" int kw_attention(int dtype, const void* qkv, int64_t B, int64_t H, in
   if (dtype == KW_DT_BF16) {
     const int64_t grid = B * H * ((T + AQ - 1) / AQ);
     if (ql2)
-      hipLaunchKernelGGL(attn_fwd_bf16<true>, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)qkv, (int)B, (int)H,
-                         (int)T, (bf16_t*)out);
+      hipLaunchKernelGGL(attn_fwd_l2, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)qkv, (int)B, (int)H, (int)T,
+                         (bf16_t*)out);
     else
-      hipLaunchKernelGGL(attn_fwd_bf16<false>, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)qkv, (int)B, (int)H,
-                         (int)T, (bf16_t*)out);
+      hipLaunchKernelGGL(attn_fwd_bf16, dim3((unsigned)grid), dim3(256), 0, s, (const bf16_t*)qkv, (int)B, (int)H, (int)T,
+                         (bf16_t*)out);
   } else if (dtype == KW_DT_F32) {
     const int64_t grid = B * H * ((T + 3) / 4);
     hipLaunchKernelGGL(attn_fwd_f32, dim3((unsigned)grid), dim3(256), 0, s, (const float*)qkv, (int)B, (int)H, (int)T,

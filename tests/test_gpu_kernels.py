@@ -333,6 +333,29 @@ def test_attention_bf16_q_log2(B, H, T):
     torch.testing.assert_close(nat.float(), _ref_attn(qkv, B, H, T, hd), atol=3e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("B,H,T,ramp", [(2, 4, 1500, 40.0), (1, 3, 130, 60.0), (1, 2, 64, 20.0), (1, 2, 50, 0.0),
+                                         (1, 2, 1, 0.0)])
+def test_attention_bf16_q_log2_reference_moves(B, H, T, ramp):
+    """attn_fwd_l2 computes p = exp2(s) before knowing whether the tile moves the exponent reference and redoes
+    the tile only when some lane's row sum exceeds e^8: key scores that grow along the sequence make the
+    reference move again and again (the rare branch in most tiles), a tile of <= 64 keys is both first and
+    ragged, T = 1 has one key.  Within bf16 rounding of fp32 softmax(q k^T) v; the r03x lab run held it bitwise
+    equal to the always-compute-the-maximum kernel it replaced (tools/lab/enc_attn_l2_ab.py)."""
+    hd = 64
+    g = torch.Generator(device="cuda").manual_seed(7)
+    qkv = torch.randn(3, B, H, T, hd, device="cuda", generator=g) * 0.5
+    qkv[0] *= 0.125 * 8 * 1.4426950408889634
+    qkv[1] *= (1.0 + ramp * torch.arange(T, device="cuda", dtype=torch.float32) / T)[None, None, :, None]
+    q2 = qkv.bfloat16()
+    out = torch.full((B, T, H * hd), float("nan"), device="cuda", dtype=torch.bfloat16)
+    ops.attention(q2, B, H, T, hd, out, q_log2=True)
+    ref_q = q2.float().clone()
+    ref_q[0] /= 1.4426950408889634
+    ref = _ref_attn(ref_q, B, H, T, hd)
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.float(), ref, atol=3e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("B,H,T", [(2, 3, 100), (1, 6, 1500)])
 def test_attention_f32(B, H, T):
     hd = 64

@@ -34,7 +34,7 @@ def main(path):
         print(f"  {k:60s} n={c:4d} total {tot / 1e3:9.1f} us  mean {tot / c / 1e3:8.1f} us  {100 * tot / busy:5.1f} %")
     # the encoder GEMMs in order within one layer (after the first attention)
     names = [r[0].split("(")[0] for r in seq]
-    a = names.index("attn_fwd_bf16")
+    a = next(j for j, n in enumerate(names) if n.startswith("attn_fwd"))
     print("one layer:", [(names[j][:26], round((seq[j][2] - seq[j][1]) / 1e3, 1)) for j in range(a - 2, a + 6)])
 
 
