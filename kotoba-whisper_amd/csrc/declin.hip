@@ -68,7 +68,7 @@ struct DecP {
   int M, N, K;
   float* slab;
   int* cnt;
-  int xlds;  // stage the activation rows through LDS (single-round, no-split-K grids)
+  int xlds;  // stage the activation rows through LDS (single-round grids and split-K slices)
 };
 
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
@@ -869,10 +869,11 @@ Geo choose(int64_t N, int64_t K) {
 }
 
 // LDS staging pays where one round of workgroups covers the grid (its 80-114 KB of LDS allows one
-// workgroup per CU) and K is not split (split-K workgroups read short row pieces); the LM head's
+// workgroup per CU) and for the split-K workgroups (fc2: each stages its 32 rows x 864-element slice, 55 KB,
+// two workgroups per CU: 10.3 vs 10.7 us, bitwise equal, profiles/r03_lab_notes.md r03y); the LM head's
 // 1,621-workgroup grid keeps direct fragment loads at four workgroups per CU.
-bool use_xlds(int64_t N, const Geo& g) { return g.ks == 1 && (N + 16 * g.ncb - 1) / (16 * g.ncb) <= 256; }
-size_t x_lds_bytes_for(int nkt, bool xlds) { return xlds ? x_lds_bytes(nkt) : 0; }
+bool use_xlds(int64_t N, const Geo& g) { return g.ks > 1 || (N + 16 * g.ncb - 1) / (16 * g.ncb) <= 256; }
+size_t x_lds_bytes_for(int nkt, int ks, bool xlds) { return xlds ? x_lds_bytes((nkt + ks - 1) / ks) : 0; }
 
 int device_cus() {
   static int ncu = 0;
@@ -896,7 +897,7 @@ hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
                        dim3((unsigned)(64 * g.nw)), 0, s, p, zper);
     return hipGetLastError();
   }
-  const size_t shm = x_lds_bytes_for(nkt, p.xlds);
+  const size_t shm = x_lds_bytes_for(nkt, g.ks, p.xlds);
   static size_t attr = 0;  // dynamic LDS this instantiation is cleared for
   if (shm > attr) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dec_linear_kernel<KTM, NCB, LNA, EPI, TC>),
