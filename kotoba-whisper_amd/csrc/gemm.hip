@@ -520,7 +520,16 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
               o.y = pack_bf16x2(v[2], v[3]);
               o.z = pack_bf16x2(v[4], v[5]);
               o.w = pack_bf16x2(v[6], v[7]);
-              *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = o;
+              // non-temporal where the consumer is compute-bound (head-split q/k/v and cross K/V for the attention,
+              // fc1's GELU output for fc2): the tile's 128 KB of stores then do not evict the operand panels the next
+              // tiles re-read (tools/gemm_bench.py, r03z: QKV 500 -> 465-484, fc1 621 -> 590, cross K/V 9.3 -> 8.2 ms);
+              // the out-proj / fc2 deltas stay cacheable for the HBM-bound LayerNorm that reads them next
+              const bool nt = EPI == KW_EPI_HEADSPLIT || p.gelu;
+              typedef __attribute__((ext_vector_type(4))) unsigned int nt_u4;
+              if (nt)
+                __builtin_nontemporal_store(nt_u4{o.x, o.y, o.z, o.w}, reinterpret_cast<nt_u4*>(reinterpret_cast<bf16_t*>(p.C) + off));
+              else
+                *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(p.C) + off) = o;
             }
           }
         }
