@@ -844,7 +844,7 @@ __device__ __forceinline__ void wave_partials_combine(unsigned long long* gr, in
       }
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(KW_POLL_SLEEP);
   }
   float M = -INFINITY, Lr = 0.f, A = 0.f;
 #pragma unroll
@@ -1120,7 +1120,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void x
       }
       continue;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(KW_POLL_SLEEP);
 #pragma unroll
     for (int i = 0; i < 4; ++i) g[i] = peek_granule(qg + sub * 4 + i);
     ok = ((g[0] & g[1] & g[2] & g[3]) >> 32) == 1ull;
@@ -1235,7 +1235,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
         }
         continue;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(KW_POLL_SLEEP);
 #pragma unroll
       for (int i = 0; i < 4; ++i) g[i] = peek_granule(qg + sub * 4 + i);
       ok = ((g[0] & g[1] & g[2] & g[3]) >> 32) == 1ull;

@@ -14,6 +14,10 @@ typedef uint16_t bf16_t;  // storage type for bf16 in global memory
 
 #define KW_WAVE 64
 
+#ifndef KW_POLL_SLEEP
+#define KW_POLL_SLEEP 1  // s_sleep units (64 cycles) between the polls of an in-launch hand-off
+#endif
+
 __device__ __forceinline__ float bf2f(bf16_t v) {
   return __uint_as_float(((uint32_t)v) << 16);
 }

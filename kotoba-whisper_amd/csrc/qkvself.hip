@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void q
     for (;; ++it) {
       x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if ((x >> 32) == 1ull || it >= QS_SPIN_LIMIT) break;
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(KW_POLL_SLEEP);
     }
     if ((x >> 32) != 1ull || !len_ok) {
       x = 0x7fc07fc0ull;  // bf16 NaN pair: the failure propagates to the output
