@@ -67,6 +67,15 @@ def kernel_source_hash() -> str:
     return h.hexdigest()
 
 
+def profile_tag_order(path: str):
+    """Sort key of a profiles/ file by its run tag: r01 < r01j < r01z < r01aa < r02 < r10 (numeric round, then the
+    letter suffix a..z, aa..az, ...: shorter suffixes first)."""
+    import re
+
+    m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
+    return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+
+
 def pmc_traffic(kernel: str):
     """HBM bytes per launch of ``kernel`` from the newest committed rocprofv3 FETCH_SIZE summary
     (profiles/rNN[x]_pmc_fetch.csv, written by tools/profile.sh + tools/rocpd_summary.py): FETCH_SIZE is
@@ -78,11 +87,7 @@ def pmc_traffic(kernel: str):
     import glob
     import re
 
-    def order(path):  # r01 < r01j < r02 < r10 (numeric round, then the letter suffix)
-        m = re.match(r"r(\d+)([a-z]*)_", os.path.basename(path))
-        return (int(m.group(1)), m.group(2)) if m else (-1, "")
-
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch.csv")), key=order)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch.csv")), key=profile_tag_order)
     if not files:
         return None, "no PMC pass committed"
     newest = files[-1]

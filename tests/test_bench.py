@@ -49,3 +49,13 @@ def test_kernel_source_hash_covers_product_sources_only(tmp_path):
         assert bench.kernel_source_hash() == h  # a file outside the Makefile's SRCS does not change it
     finally:
         os.remove(scratch)
+
+
+def test_pmc_pass_order_by_run_tag():
+    """pmc_traffic() reads the newest committed PMC pass: run tags sort by round, then by suffix a..z, aa, ab, ..."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    tags = ["r10_x", "r03ad_x", "r01_x", "r03w_x", "r01aa_x", "r01z_x", "r01j_x", "r03_x"]
+    assert sorted(tags, key=bench.profile_tag_order) == ["r01_x", "r01j_x", "r01z_x", "r01aa_x", "r03_x", "r03w_x",
+                                                          "r03ad_x", "r10_x"]
