@@ -90,6 +90,57 @@ def test_tiny_bf16_beam_runs(gold, tiny16):
     assert toks.min() >= 0 and toks.max() < TINY.vocab_size
 
 
+def _tf_logprobs(eng, enc_row, seq, P):
+    """Per-token log-softmax of the teacher-forced logits of ``seq`` (prompt + generated) at positions P.."""
+    sess = eng.new_session(1, enc_row)
+    t = torch.as_tensor(seq, dtype=torch.int64)[None]
+    lg = sess.teacher_forced_logits(t, P)[0, : t.shape[1] - P].float()
+    lp = torch.log_softmax(lg, -1)
+    return lp.gather(-1, t[0, P:].cuda()[:, None])[:, 0].double().cpu().numpy()
+
+
+@pytest.mark.parametrize("mode", ["beam3_eos", "beam2_eos_never"])
+def test_tiny_bf16_beam_rescored(gold, tiny32, tiny16, mode):
+    """bf16 beam search with beams that finish on EOS (length penalty 1.0 / 2.0, early_stopping False / "never"):
+    every item's chosen hypothesis, rescored by the fp32 engine (bit-exact to HF beam search above) with HF's
+    finished-beam score -- sum of log-probs / generated_len ** length_penalty (TF/generation/utils.py:3182) --
+    is as good as HF fp32's choice within the bf16 scoring noise of the two hypotheses."""
+    g = gold("tiny_beam_fp32")
+    kw, eos = BEAM_MODES[mode]
+    gen = generation_constants(TINY)
+    gen.eos_token_id = eos
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
+    t16 = tiny16.generate(feats, generation_config=gen, **kw).cpu().numpy()
+    t32 = g[f"{mode}_tokens"]
+    prompt = [gen.decoder_start_token_id, gen.lang_to_id["<|ja|>"], gen.task_to_id["transcribe"],
+              gen.no_timestamps_token_id]
+    P, max_new, lp_pen = len(prompt), kw["max_length"], kw.get("length_penalty", 1.0)
+    e32 = tiny32.engine.encode(feats).view(4, 1500, -1)
+    e16 = tiny16.engine.encode(feats).view(4, 1500, -1)
+
+    def hyp(row):
+        r = [int(x) for x in row]
+        while r and r[-1] == gen.pad_token_id:
+            r.pop()
+        return prompt + r + ([eos] if len(r) < max_new else [])
+
+    same = 0
+    for b in range(4):
+        h16, h32 = hyp(t16[b]), hyp(t32[b])
+        s = {}
+        for name, h in (("h16", h16), ("h32", h32)):
+            lp32 = _tf_logprobs(tiny32.engine, e32[b].reshape(1500, -1), h, P)
+            lp16 = _tf_logprobs(tiny16.engine, e16[b].reshape(1500, -1), h, P)
+            n = len(h) - P
+            s[name] = (lp32.sum() / n ** lp_pen, lp16.sum() / n ** lp_pen)
+        tol = abs(s["h16"][1] - s["h16"][0]) + abs(s["h32"][1] - s["h32"][0]) + 1e-4
+        same += h16 == h32
+        print(f"\ntiny bf16 {mode} item {b}: same hypothesis {h16 == h32}; fp32 score of the bf16 choice "
+              f"{s['h16'][0]:.5f} vs HF fp32's {s['h32'][0]:.5f} (tolerance {tol:.5f})")
+        assert s["h16"][0] >= s["h32"][0] - tol
+    print(f"tiny bf16 {mode}: {same}/4 items chose HF fp32's hypothesis")
+
+
 def test_tiny_fp32_logits(gold, tiny32):
     g = gold("tiny_fp32")
     feats = torch.from_numpy(oracle_features(TINY, g["cases"])).cuda()
