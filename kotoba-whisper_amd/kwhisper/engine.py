@@ -34,7 +34,7 @@ def _to_tensor(v) -> torch.Tensor:
 
 
 class _EncoderBuffers:
-    def __init__(self, eng: "WhisperEngine", B: int):
+    def __init__(self, eng: "WhisperEngine", B: int, out: torch.Tensor | None = None):
         s, dev, dt = eng.shape, eng.device, eng.dtype
         d, T = s.d_model, s.max_source_positions
         self.B = B
@@ -47,7 +47,7 @@ class _EncoderBuffers:
         self.qkv = torch.empty((3 * B * T * d,), device=dev, dtype=dt)
         self.attn = torch.empty((B * T, d), device=dev, dtype=dt)
         self.ffn = torch.empty((B * T, s.encoder_ffn_dim), device=dev, dtype=dt)
-        self.out = torch.empty((B * T, d), device=dev, dtype=dt)
+        self.out = torch.empty((B * T, d), device=dev, dtype=dt) if out is None else out
         # bf16 path: out-proj / fc2 store their output here and the next LayerNorm adds it into h
         # (a bf16 store is cheaper than the f32 read-modify-write of a residual epilogue)
         self.delta = torch.empty((B * T, d), device=dev, dtype=dt) if dt == torch.bfloat16 else None
@@ -63,7 +63,7 @@ class WhisperEngine:
 
     def __init__(self, shape: WhisperShape, state_dict: dict, *, dtype=torch.bfloat16, device="cuda",
                  generation_config: GenerationConstants | None = None, fuse_qkv_self: bool = True,
-                 fuse_xq_cross: bool = True):
+                 fuse_xq_cross: bool = True, encoder_streams: int = 2):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
         L.load()
@@ -76,6 +76,11 @@ class WhisperEngine:
         # ... and each layer's cross-attention query projection + cross-attention step as one kw_dec_xq_cross launch
         # (bitwise the two-launch plan; False keeps the two launches)
         self.fuse_xq_cross = bool(fuse_xq_cross)
+        # the encoder's batch as this many parts, their kernels issued interleaved on as many side streams: each
+        # GEMM's last round of 256-row tiles leaves CUs idle that the other part's kernels fill (rows are
+        # independent, so the output is bitwise the one-pass encoder's; large-v3 B = 32: 70.5 -> 67.6 ms,
+        # profiles/r03_lab_notes.md r03ag)
+        self.encoder_streams = max(1, int(encoder_streams))
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("WhisperEngine runs on a cuda (HIP) device only")
@@ -87,6 +92,8 @@ class WhisperEngine:
         self.c_pad = (-(-shape.num_mel_bins // 64) * 64) if dtype == torch.bfloat16 else (-(-shape.num_mel_bins // 16) * 16)
         self._load(state_dict)
         self._enc = {}
+        self._enc_split = {}
+        self._enc_streams = []
 
     # ------------------------------------------------------------------------------------------
     def _dev(self, t: torch.Tensor, dtype=None) -> torch.Tensor:
@@ -250,18 +257,57 @@ class WhisperEngine:
             )
         mel = mel.to(device=self.device, dtype=torch.float32).contiguous()
         B = mel.shape[0]
+        parts = min(self.encoder_streams, B)
+        if parts > 1:
+            return self._encode_split(mel, parts)
         bf = self.encoder_buffers(B)
         ops.mel_to_time_major(mel, self.c_pad, self.dtype, out=bf.mel_tm)
-        T = s.max_source_positions
         for p in bf.plans:
-            if isinstance(p, tuple):
-                if p[0] == "ln":
-                    ops.layernorm(p[1], p[2], p[3], s.layer_norm_eps, p[4], delta=p[5])
-                else:
-                    ops.attention(p[1], B, self.H, T, _HD, p[2], q_log2=p[3])
-            else:
-                p()
+            self._enc_op(p, B)
         return bf.out
+
+    def _enc_op(self, p, B: int) -> None:
+        if isinstance(p, tuple):
+            if p[0] == "ln":
+                ops.layernorm(p[1], p[2], p[3], self.shape.layer_norm_eps, p[4], delta=p[5])
+            else:
+                ops.attention(p[1], B, self.H, self.shape.max_source_positions, _HD, p[2], q_log2=p[3])
+        else:
+            p()
+
+    def _encode_split(self, mel: torch.Tensor, parts: int) -> torch.Tensor:
+        """encode() over ``parts`` row blocks of the batch, each with its own buffers and side stream, their
+        launches issued in lockstep (plan i of every part, then plan i + 1) so that one part's kernels run in
+        the CUs another part's kernel leaves idle.  Each part writes its rows of one (B*T, d) output."""
+        s, B = self.shape, mel.shape[0]
+        T, d = s.max_source_positions, s.d_model
+        sizes = [B // parts + (1 if i < B % parts else 0) for i in range(parts)]
+        key = (B, parts)
+        if key not in self._enc_split:
+            out = torch.empty((B * T, d), device=self.device, dtype=self.dtype)
+            bufs, r0 = [], 0
+            for n in sizes:
+                bufs.append(_EncoderBuffers(self, n, out=out[r0 * T:(r0 + n) * T]))
+                r0 += n
+            self._enc_split[key] = (out, bufs)
+        out, bufs = self._enc_split[key]
+        while len(self._enc_streams) < parts:
+            self._enc_streams.append(torch.cuda.Stream(device=self.device))
+        streams = self._enc_streams[:parts]
+        cur = torch.cuda.current_stream(self.device)
+        r0 = 0
+        for bf, st, n in zip(bufs, streams, sizes):
+            st.wait_stream(cur)
+            with torch.cuda.stream(st):
+                ops.mel_to_time_major(mel[r0:r0 + n], self.c_pad, self.dtype, out=bf.mel_tm)
+            r0 += n
+        for j in range(len(bufs[0].plans)):
+            for bf, st in zip(bufs, streams):
+                with torch.cuda.stream(st):
+                    self._enc_op(bf.plans[j], bf.B)
+        for st in streams:  # (the join also orders any later reuse of mel's memory after the parts' reads)
+            cur.wait_stream(st)
+        return out
 
     # ------------------------------------------------------------------------------------------
     def cross_kv(self, enc: torch.Tensor, B: int, out: torch.Tensor | None = None) -> torch.Tensor:
