@@ -74,6 +74,8 @@ class DecodeSession:
         self.samp_ws = torch.zeros((ops.greedy_step_workspace_bytes(R) + 3) // 4, device=dev, dtype=torch.float32)
         self._greedy_cfg = {}
         self._pinned = None
+        # greedy prefill as two row blocks on two side streams (generate(); bitwise the one-pass prefill)
+        self.prefill_streams = 2
         if enc is not None:
             self.set_encoder_output(enc)
 
@@ -86,6 +88,54 @@ class DecodeSession:
             return
         self.eng.cross_kv(enc, self.B, out=self.cross)
         self._cross_key = key
+
+    def _row_view(self, r0: int, r1: int) -> "DecodeSession":
+        """A session over greedy rows [r0, r1) of this one: its ids / caches / cross K/V / logits are row slices
+        of this session's, its activation buffers and launch workspaces its own (so two views can run at once).
+        Every decode op's per-row arithmetic is independent of the other rows, so a view computes bitwise what
+        the full session computes for those rows."""
+        v = object.__new__(DecodeSession)
+        v.eng, v.nb, v.B, v.R, v.T = self.eng, 1, r1 - r0, r1 - r0, self.T
+        v.cross, v.kc, v.vc = self.cross[:, r0:r1], self.kc[:, r0:r1], self.vc[:, r0:r1]
+        v.ids, v.bp, v.cur_len, v.logits = self.ids[r0:r1], None, self.cur_len, self.logits[r0:r1]
+        v._bufs, v._plans = {}, {}
+        v.lin_ws = torch.zeros_like(self.lin_ws) if self.lin_ws is not None else None
+        v.self_ws = torch.zeros_like(self.self_ws)
+        v.qs_ok = v.xc_ok = False
+        v.qs_ws = v.xc_ws = None
+        return v
+
+    def _prefill_parts(self, parts: int):
+        """Row views for a prefill split over ``parts`` side streams (greedy rows only), cached."""
+        key = ("views", parts)
+        if key not in self._plans:
+            R = self.R
+            sizes = [R // parts + (1 if i < R % parts else 0) for i in range(parts)]
+            views, r0 = [], 0
+            for n in sizes:
+                views.append(self._row_view(r0, r0 + n))
+                r0 += n
+            self._plans[key] = (views, [torch.cuda.Stream(device=self.eng.device) for _ in range(parts)])
+        return self._plans[key]
+
+    def _run_prefill(self, P: int, parts: int) -> None:
+        """The prompt's forward pass (prefill) as ``parts`` row blocks on side streams, their launches issued in
+        lockstep: each block's kernels are latency-bound chains on few CUs, and two of them overlap (the
+        encoder's split, engine._encode_split).  Joined on the current stream before the sampler."""
+        if parts <= 1 or self.nb != 1 or self.R < 2 * parts:
+            self._run(self._step_plans(P))
+            return
+        views, streams = self._prefill_parts(parts)
+        seqs = [v._step_plans(P) for v in views]
+        cur = torch.cuda.current_stream(self.eng.device)
+        for st in streams:
+            st.wait_stream(cur)
+        for j in range(len(seqs[0])):
+            for v, seq, st in zip(views, seqs, streams):
+                with torch.cuda.stream(st):
+                    v._run([seq[j]])
+        for st in streams:
+            cur.wait_stream(st)
 
     def _buffers(self, q: int):
         if q not in self._bufs:
@@ -253,7 +303,8 @@ class DecodeSession:
         # a repeat call (the next batch) replays the same graph (no re-capture)
         key = (max_length, P, bool(return_timestamps), tuple(gen.suppress_tokens or ()),
                tuple(gen.begin_suppress_tokens or ()), gen.timestamp_begin, gen.no_timestamps_token_id,
-               gen.eos_token_id, gen.pad_token_id, gen.max_initial_timestamp_index, bool(record_scores))
+               gen.eos_token_id, gen.pad_token_id, gen.max_initial_timestamp_index, bool(record_scores),
+               self.prefill_streams)
         cfg = self._greedy_cfg.get(key)
         if cfg is None:
             sup = torch.zeros((self.eng.shape.vocab_size,), dtype=torch.uint8)
@@ -279,7 +330,7 @@ class DecodeSession:
         # prefill (replayed from a graph cached with the configuration: ~260 launches otherwise go
         # through Python one by one)
         def prefill():
-            self._run(self._step_plans(P))
+            self._run_prefill(P, self.prefill_streams)
             sampler()
 
         pg = cfg.get("prefill_graph")
