@@ -74,8 +74,6 @@ class DecodeSession:
         self.samp_ws = torch.zeros((ops.greedy_step_workspace_bytes(R) + 3) // 4, device=dev, dtype=torch.float32)
         self._greedy_cfg = {}
         self._pinned = None
-        # greedy prefill as two row blocks on two side streams (generate(); bitwise the one-pass prefill)
-        self.prefill_streams = 2
         if enc is not None:
             self.set_encoder_output(enc)
 
@@ -304,7 +302,7 @@ class DecodeSession:
         key = (max_length, P, bool(return_timestamps), tuple(gen.suppress_tokens or ()),
                tuple(gen.begin_suppress_tokens or ()), gen.timestamp_begin, gen.no_timestamps_token_id,
                gen.eos_token_id, gen.pad_token_id, gen.max_initial_timestamp_index, bool(record_scores),
-               self.prefill_streams)
+               self.eng.prefill_streams)
         cfg = self._greedy_cfg.get(key)
         if cfg is None:
             sup = torch.zeros((self.eng.shape.vocab_size,), dtype=torch.uint8)
@@ -330,7 +328,7 @@ class DecodeSession:
         # prefill (replayed from a graph cached with the configuration: ~260 launches otherwise go
         # through Python one by one)
         def prefill():
-            self._run_prefill(P, self.prefill_streams)
+            self._run_prefill(P, self.eng.prefill_streams)
             sampler()
 
         pg = cfg.get("prefill_graph")

@@ -368,3 +368,42 @@ def test_fused_decode_blocks_generate(gold):
     print(f"fused vs two-launch: {compared} tokens compared; teacher-forced logits max diff {diff.max().item():.4g} "
           f"mean {diff.mean().item():.3g} (range {lb.abs().max().item():.3g})")
     assert diff.max().item() < 0.1 and diff.mean().item() < 0.01  # measured: max 0.025, mean 0.0015
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_encoder_streams_bitwise(tiny16, tiny32, dtype):
+    """The encoder as row blocks on side streams (engine.encoder_streams, default 2; engine._encode_split) writes
+    bitwise the one-pass encoder's rows -- also for a batch that does not split evenly (B = 5: 3 + 2 rows)."""
+    eng = (tiny16 if dtype == torch.bfloat16 else tiny32).engine
+    g = torch.Generator(device="cuda").manual_seed(11)
+    mel = torch.randn(5, TINY.num_mel_bins, TINY.n_frames, device="cuda", generator=g) * 0.5
+    old = eng.encoder_streams
+    try:
+        eng.encoder_streams = 1
+        ref = eng.encode(mel).clone()
+        for parts in (2, 3):
+            eng.encoder_streams = parts
+            got = eng.encode(mel)
+            torch.cuda.synchronize()
+            assert torch.equal(got.view(torch.int16) if dtype == torch.bfloat16 else got,
+                               ref.view(torch.int16) if dtype == torch.bfloat16 else ref), parts
+    finally:
+        eng.encoder_streams = old
+
+
+@pytest.mark.parametrize("ts", [False, True])
+def test_prefill_streams_tokens_identical(tiny16, ts):
+    """The greedy prefill as two row views on side streams (WhisperEngine.prefill_streams, default 2) gives
+    generate() exactly the one-pass prefill's tokens (B = 6: two views of 3 rows), with and without timestamps."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    feats = torch.randn(6, TINY.num_mel_bins, TINY.n_frames, device="cuda", generator=g) * 0.5
+    kw = dict(language="ja", task="transcribe", return_timestamps=ts, max_length=24)
+    out = {}
+    eng = tiny16.engine
+    try:
+        for parts in (2, 1):
+            eng.prefill_streams = parts
+            out[parts] = tiny16.generate(feats, **kw).cpu()
+    finally:
+        eng.prefill_streams = 2
+    assert torch.equal(out[1], out[2])

@@ -1,5 +1,5 @@
 """r03ah lab: the greedy prefill (4-token prompt, large-v3, B = 32) as one pass vs two row blocks on two side
-streams (DecodeSession.prefill_streams): token ids of generate() bitwise, and the captured prefill graph's replay
+streams (WhisperEngine.prefill_streams): token ids of generate() bitwise, and the captured prefill graph's replay
 time (HIP events, alternating rounds)."""
 import os
 import sys
@@ -26,22 +26,17 @@ audio = torch.from_numpy(np.stack([dummy_audio(i) for i in range(B)])).to(dev)
 feats = fe.extract(audio)
 kw = dict(language="ja", task="transcribe", max_length=128, return_timestamps=False)
 ids = {}
-sess = None
+eng = model.engine
 for parts in (1, 2, 1, 2):
-    if sess is not None:
-        sess.prefill_streams = parts
-    out = model.generate(feats, **kw).cpu()
-    sess = model._sessions.get((B, 1)) or model._sessions[(B, 1, 1)]
-    if sess.prefill_streams != parts:  # the first call made the session: run again with the setting
-        sess.prefill_streams = parts
-        out = model.generate(feats, **kw).cpu()
-    ids.setdefault(parts, []).append(out)
+    eng.prefill_streams = parts
+    ids.setdefault(parts, []).append(model.generate(feats, **kw).cpu())
+sess = model._sessions.get((B, 1)) or model._sessions[(B, 1, 1)]
 print("ids equal across runs / settings:", all(torch.equal(ids[1][0], x) for x in ids[1] + ids[2]), tuple(ids[1][0].shape),
       flush=True)
 best = {}
 for _ in range(5):
     for parts in (1, 2):
-        sess.prefill_streams = parts
+        eng.prefill_streams = parts
         model.generate(feats, **kw)
         pg = next(c["prefill_graph"] for k, c in sess._greedy_cfg.items() if k[-1] == parts and c.get("prefill_graph"))
         torch.cuda.synchronize()
