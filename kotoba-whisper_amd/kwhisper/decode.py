@@ -358,36 +358,56 @@ class DecodeSession:
             self._run(step_seq)
             sampler()
 
-        graph = cfg["graph"]
-        if graph is None and use_graph and not record_scores and n_steps > 1:
-            graph = torch.cuda.CUDAGraph()
+        def capture(n):
+            g = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.graph(graph, stream=side):
-                one_step()
+            with torch.cuda.graph(g, stream=side):
+                for _ in range(n):
+                    one_step()
             torch.cuda.current_stream(dev).wait_stream(side)
-            cfg["graph"] = graph
+            return g
+
+        graph = cfg["graph"]
+        if graph is None and use_graph and not record_scores and n_steps > 1:
+            graph = cfg["graph"] = capture(1)
+        # K (engine.steps_per_replay) steps per replay where K steps remain: one replay launch, unfinished-count
+        # copy and event per K steps; every step reads its position from the device, so K steps in one graph are
+        # the same K replays of the one-step graph
+        K = max(1, int(self.eng.steps_per_replay))
+        graph_k = cfg.get(("graph", K)) if K > 1 else None
+        if K > 1 and graph_k is None and graph is not None and n_steps > K:
+            graph_k = cfg[("graph", K)] = capture(K)
         if not use_graph:
-            graph = None
+            graph = graph_k = None
         self._graph, self._graph_key = graph, key
         if self._pinned is None or self._pinned.numel() < check_every + 1:
             self._pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
         pinned = self._pinned
         events = []
+        lag = max(1, check_every // K) if graph_k is not None else check_every  # the same lag in steps
         while done < n_steps:
-            if graph is not None:
-                graph.replay()
+            if graph_k is not None and done + K <= n_steps:
+                graph_k.replay()
+                done += K
             else:
-                one_step()
+                if graph is not None:
+                    graph.replay()
+                else:
+                    one_step()
+                done += 1
             if record_scores:
                 self.scores.append((self.logits.clone(), score_buf.clone()))
-            done += 1
-            slot = done % (check_every + 1)
+            slot = done % (check_every + 1)  # (distinct over the lag + 1 copies in flight)
+            # a sentinel first: the stop test trusts only a count the copy actually delivered (r03al: a fresh
+            # pinned buffer read as 0 -- "all rows finished" -- after its event had completed but before the 4-byte
+            # D2H copy's write was visible to the host, ending the loop early); a count of 0 from any step is final
+            pinned[slot] = -1
             pinned[slot : slot + 1].copy_(self.n_unfinished, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()
             events.append((ev, slot))
-            if len(events) > check_every:
+            if len(events) > lag:
                 e0, s0 = events.pop(0)
                 e0.synchronize()
                 if int(pinned[s0]) == 0:
@@ -508,6 +528,7 @@ class DecodeSession:
                 one_step()
             n += 1
             slot = n % (check_every + 1)
+            pinned[slot] = -1  # sentinel: only a delivered 0 stops the loop (see generate)
             pinned[slot: slot + 1].copy_(st["go"], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record()

@@ -63,7 +63,8 @@ class WhisperEngine:
 
     def __init__(self, shape: WhisperShape, state_dict: dict, *, dtype=torch.bfloat16, device="cuda",
                  generation_config: GenerationConstants | None = None, fuse_qkv_self: bool = True,
-                 fuse_xq_cross: bool = True, encoder_streams: int = 2, prefill_streams: int = 2):
+                 fuse_xq_cross: bool = True, encoder_streams: int = 2, prefill_streams: int = 2,
+                 steps_per_replay: int = 2):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
         L.load()
@@ -84,6 +85,9 @@ class WhisperEngine:
         # ... and the greedy prefill (the prompt's pass) as this many row views of the session on side streams
         # (DecodeSession._run_prefill; tokens identical; 5.65 -> 5.2 ms at large-v3 B = 32, r03ah)
         self.prefill_streams = max(1, int(prefill_streams))
+        # greedy decode steps per hipGraph replay (DecodeSession.generate: one launch, one unfinished-count copy and
+        # event per replay; the host's stop check keeps the same lag in steps)
+        self.steps_per_replay = max(1, int(steps_per_replay))
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("WhisperEngine runs on a cuda (HIP) device only")

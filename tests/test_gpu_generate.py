@@ -407,3 +407,25 @@ def test_prefill_streams_tokens_identical(tiny16, ts):
     finally:
         eng.prefill_streams = 2
     assert torch.equal(out[1], out[2])
+
+
+@pytest.mark.parametrize("ts,eos", [(False, None), (True, None), (False, 7656)])
+def test_steps_per_replay_tokens_identical(tiny16, ts, eos):
+    """Two greedy steps per hipGraph replay (WhisperEngine.steps_per_replay, default 2) give exactly the tokens of
+    one step per replay -- also when rows finish early on EOS (the host stop check's lag is kept in steps) and for
+    an odd number of remaining steps (max_length 25: the last step replays the one-step graph)."""
+    g = torch.Generator(device="cuda").manual_seed(9)
+    feats = torch.randn(6, TINY.num_mel_bins, TINY.n_frames, device="cuda", generator=g) * 0.5
+    gen = generation_constants(TINY)
+    if eos is not None:
+        gen.eos_token_id = eos
+    kw = dict(language="ja", task="transcribe", return_timestamps=ts, max_length=25, generation_config=gen)
+    out = {}
+    eng = tiny16.engine
+    try:
+        for k in (2, 1, 3):
+            eng.steps_per_replay = k
+            out[k] = tiny16.generate(feats, **kw).cpu()
+    finally:
+        eng.steps_per_replay = 2
+    assert torch.equal(out[1], out[2]) and torch.equal(out[1], out[3])
