@@ -289,7 +289,7 @@ class WhisperEngine:
         s, B = self.shape, mel.shape[0]
         T, d = s.max_source_positions, s.d_model
         sizes = [B // parts + (1 if i < B % parts else 0) for i in range(parts)]
-        key = (B, parts)
+        key = (B, tuple(sizes))
         if key not in self._enc_split:
             out = torch.empty((B * T, d), device=self.device, dtype=self.dtype)
             bufs, r0 = [], 0
