@@ -59,3 +59,17 @@ for rnd in range(8):
 print("output unchanged:", torch.equal(out, ref))
 for f in fracs:
     print(f"pre-read {f:4.0%} of K/V rows: prefetch {pre[f]:7.1f} us, xq_cross {best[f]:6.2f} us (best of 7)", flush=True)
+
+# residency check: the same default-policy read of 75 % of K (92 MB) right after a flush, then again
+half = cross[0, :24]
+for rnd in range(4):
+    sink[0] += flush.sum(dtype=torch.float32)
+    ts = []
+    for _ in range(2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        sink[3] += half.sum(dtype=torch.float32)
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3)
+    print(f"92 MB default-policy read: cold {ts[0]:6.1f} us, repeated {ts[1]:6.1f} us", flush=True)
