@@ -94,9 +94,9 @@ __global__ __launch_bounds__(ST) void greedy_step_kernel(kw_sampler_args a) {
 
 // Split-row variant (no timestamps, no scores_out): row b's V logits are cut into NSPLIT slices of one
 // 512-thread workgroup each (16 loads in flight per thread: one memory round trip per slice instead of
-// a serial walk over the row); each slice publishes its (max, first index) write-through, and the row's
-// last arriver combines the slices in slice order (first index on ties, as torch.argmax) and finishes
-// the step exactly as greedy_step_kernel does.
+// a serial walk over the row); each slice publishes its (max, first index, finished flag) write-through,
+// and the last of all B x NSPLIT workgroups to arrive combines every row's slices in slice order (first
+// index on ties, as torch.argmax) and finishes the step exactly as greedy_step_kernel does.
 constexpr int SPLIT_T = 512, NSPLIT = 8, SUNR = 16, PART = 8;  // PART: floats published per slice
 
 __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_kernel(kw_sampler_args a) {
@@ -160,45 +160,55 @@ __global__ __launch_bounds__(SPLIT_T) void greedy_step_split_kernel(kw_sampler_a
   }
   if ((tid & 63) == 0) { shf[tid >> 6] = best; shi[tid >> 6] = bi; }
   fin = __syncthreads_or(fin);
-  if (tid != 0) return;
-  for (int i = 1; i < SPLIT_T / 64; ++i)
-    if (shf[i] > best || (shf[i] == best && shi[i] < bi)) { best = shf[i]; bi = shi[i]; }
-  float* part = reinterpret_cast<float*>(a.workspace) + ((int64_t)b * NSPLIT + sl) * PART;
-  int* rcnt = reinterpret_cast<int*>(a.workspace) + (int64_t)a.B * NSPLIT * PART + b;
-  __hip_atomic_store(part, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(reinterpret_cast<int*>(part) + 1, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int prev = __hip_atomic_fetch_add(rcnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (prev != NSPLIT - 1) return;
-  __hip_atomic_store(rcnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const float* row = reinterpret_cast<const float*>(a.workspace) + (int64_t)b * NSPLIT * PART;
-  float pv[NSPLIT];
-  int pi[NSPLIT];
-#pragma unroll
-  for (int q = 0; q < NSPLIT; ++q) {  // every partial load in flight before the first compare
-    pv[q] = __hip_atomic_load(row + PART * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pi[q] = __hip_atomic_load(reinterpret_cast<const int*>(row) + PART * q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // one arrival count over all B x NSPLIT workgroups: the last to arrive finishes every row (a thread per
+  // row), so the step pays one atomic round trip instead of a per-row count, an ids store + fence and a
+  // second count, and the unfinished flags are summed in LDS instead of re-read
+  __shared__ int last_sh, nunf_sh;
+  if (tid == 0) {
+    nunf_sh = 0;
+    for (int i = 1; i < SPLIT_T / 64; ++i)
+      if (shf[i] > best || (shf[i] == best && shi[i] < bi)) { best = shf[i]; bi = shi[i]; }
+    float* part = reinterpret_cast<float*>(a.workspace) + ((int64_t)b * NSPLIT + sl) * PART;
+    __hip_atomic_store(part, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<int*>(part) + 1, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(reinterpret_cast<int*>(part) + 2, fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(a.counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last_sh = prev == (int)a.B * NSPLIT - 1;
   }
-  float bb = -INFINITY;
-  int ii = 0x7fffffff;
+  __syncthreads();
+  if (!last_sh) return;
+  int n_unf = 0;
+  for (int r = tid; r < (int)a.B; r += SPLIT_T) {
+    const float* row = reinterpret_cast<const float*>(a.workspace) + (int64_t)r * NSPLIT * PART;
+    float pv[NSPLIT];
+    int pi[NSPLIT], pf[NSPLIT];
 #pragma unroll
-  for (int q = 0; q < NSPLIT; ++q)  // slice order = index order: strict > keeps the first max
-    if (pv[q] > bb || (pv[q] == bb && pi[q] < ii)) { bb = pv[q]; ii = pi[q]; }
-  if (ii == 0x7fffffff) ii = 0;
-  const int64_t tok = fin ? (int64_t)a.pad_id : (int64_t)ii;
-  a.ids[(int64_t)b * a.ids_stride + L] = tok;
-  const int done = fin || tok == a.eos_id || (L + 1) >= a.max_length;
-  a.unfinished[b] = done ? 0 : 1;
-  __threadfence();
-  const int prev2 = atomicAdd(a.counter, 1);
-  if (prev2 == (int)a.B - 1) {
-    __threadfence();
-    int n = 0;
-    for (int i = 0; i < (int)a.B; ++i) n += __hip_atomic_load(a.unfinished + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *a.n_unfinished = n;
+    for (int q = 0; q < NSPLIT; ++q) {  // every partial load in flight before the first compare
+      pv[q] = __hip_atomic_load(row + PART * q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pi[q] = __hip_atomic_load(reinterpret_cast<const int*>(row) + PART * q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pf[q] = __hip_atomic_load(reinterpret_cast<const int*>(row) + PART * q + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    float bb = -INFINITY;
+    int ii = 0x7fffffff, rf = 0;
+#pragma unroll
+    for (int q = 0; q < NSPLIT; ++q) {  // slice order = index order: strict > keeps the first max
+      if (pv[q] > bb || (pv[q] == bb && pi[q] < ii)) { bb = pv[q]; ii = pi[q]; }
+      rf |= pf[q];  // (every slice scanned the same history: all equal)
+    }
+    if (ii == 0x7fffffff) ii = 0;
+    const int64_t tok = rf ? (int64_t)a.pad_id : (int64_t)ii;
+    a.ids[(int64_t)r * a.ids_stride + L] = tok;
+    const int done = rf || tok == a.eos_id || (L + 1) >= a.max_length;
+    a.unfinished[r] = done ? 0 : 1;
+    n_unf += done ? 0 : 1;
+  }
+  if (n_unf) atomicAdd(&nunf_sh, n_unf);
+  __syncthreads();
+  if (tid == 0) {
+    *a.n_unfinished = nunf_sh;
     *a.counter = 0;
     *a.cur_len = L + 1;
-    __threadfence();
   }
 }
 
