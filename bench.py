@@ -165,23 +165,23 @@ def stub_main(a, world, rank, dist):
 
     for _ in range(a.warmup):
         step()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
     ids = [step() for _ in range(a.steps)]
-    if world > 1:
-        dist.barrier()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if dist is not None:  # the ids gather is part of the timed step
         gathered = [torch.empty_like(ids[-1]) for _ in range(world)]
         dist.all_gather(gathered, ids[-1])
         assert [int(g[0, 0]) for g in gathered] == list(range(world))
+        dist.barrier()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if dist is not None:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     out = {"metric": "audio-seconds/sec (RTF) whisper-large-v3 30s@bs32", "value": world * a.batch * 30.0 * a.steps / dt,
            "unit": "audio-s/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
            "ms_per_step": dt / a.steps * 1e3, "stub": True,
-           "dist": {"world": world, "backend": dist.get_backend() if world > 1 else None}}
+           "dist": {"world": world, "backend": dist.get_backend() if dist is not None else None}}
     if rank == 0:
         print(json.dumps(out), flush=True)
 
@@ -195,11 +195,15 @@ def main(argv=None):
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     backend = os.environ.get("KW_BENCH_BACKEND", "nccl")
+    # under a launcher (torch.distributed.run sets WORLD_SIZE) the rank code always runs the distributed path --
+    # process group, barriers, max-over-ranks timing, ids gather -- world size 1 included (tests/test_gpu_dist.py
+    # runs it that way over RCCL); a plain `python bench.py` is the single-process N = 1 run
+    use_dist = "WORLD_SIZE" in os.environ
     if a.stub:
-        if world > 1:
+        if use_dist:
             dist.init_process_group(backend)
-        stub_main(a, world, rank, dist)
-        if world > 1:
+        stub_main(a, world, rank, dist if use_dist else None)
+        if use_dist:
             dist.destroy_process_group()
         return
     # one process per GPU; more ranks than GPUs only in a rehearsal (KW_BENCH_BACKEND=gloo on a 1-GPU box)
@@ -207,7 +211,7 @@ def main(argv=None):
     if ndev == 0:
         raise RuntimeError("bench.py needs a HIP device (use --stub to exercise the launcher on the CPU)")
     local = local % ndev
-    if world > 1:
+    if use_dist:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -237,29 +241,10 @@ def main(argv=None):
         for _ in range(n):
             yield model.generate(fe.extract(audio), **gen_kw)
 
-    for ids in batches(a.warmup):
-        out_ids.append(ids)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for ids in batches(a.steps):
-        out_ids.append(ids)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    dt = float(t.item())
-    new_tokens = int(out_ids[-1].shape[1])
-
-    # DP gather of the token matrices (the reference's pad_across_processes + gather_for_metrics, C4/C5)
-    ids = torch.stack(out_ids[-a.steps:]).to(torch.int32)
-    if world > 1:
+    def gather_ids(mats):
+        """DP gather of the timed batches' token matrices (the reference's pad_across_processes +
+        gather_for_metrics, C4/C5, done once for the rank's batches): width all_reduce(MAX), rows all_gather."""
+        ids = torch.stack(mats).to(torch.int32)
         L = torch.tensor([ids.shape[-1]], device=dev)
         dist.all_reduce(L, op=dist.ReduceOp.MAX)
         # padded with the tokenizer's pad id, <|endoftext|> (run_pseudo_labelling.py:339)
@@ -268,6 +253,30 @@ def main(argv=None):
         pad[..., : ids.shape[-1]] = ids
         gathered = [torch.empty_like(pad) for _ in range(world)]
         dist.all_gather(gathered, pad)
+        return gathered
+
+    for ids in batches(a.warmup):
+        out_ids.append(ids)
+    torch.cuda.synchronize()
+    if use_dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for ids in batches(a.steps):
+        out_ids.append(ids)
+    gathered = gather_ids(out_ids[-a.steps:]) if use_dist else None  # inside the timed region
+    torch.cuda.synchronize()
+    if use_dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if use_dist:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    new_tokens = int(out_ids[-1].shape[1])
+    if gathered is not None:
+        assert len(gathered) == world and all(g.shape == gathered[0].shape for g in gathered)
 
     # ---- per-kernel measurements (HIP events on the launching stream, after the timed region) ----
     eng = model.engine
@@ -365,8 +374,9 @@ def main(argv=None):
                    "max_length": a.max_length, "new_tokens": new_tokens, "seq_len": 1500,
                    "parallelism": f"dp{world}"},
         "dist": {"world": world, "rank_device": local, "device_name": torch.cuda.get_device_name(dev),
-                 "backend": dist.get_backend() if world > 1 else None,
-                 "ids_gather": "all_gather of the padded int32 token matrices" if world > 1 else None},
+                 "backend": dist.get_backend() if use_dist else None,
+                 "ids_gather": "all_gather of the padded int32 token matrices, inside the timed region"
+                 if use_dist else None},
         "roofline": {"kernel": cross_note,
                      "bound": "hbm", "achieved": cross_bytes / cross_t / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": cross_bytes / cross_t / 1e9 / HBM_PEAK_GBS, "traffic": None,
@@ -397,7 +407,7 @@ def main(argv=None):
                       f"greedy, {cb['new_tokens']} new tokens, {cb['seconds']:.1f} s; run_speed_eval.py:73-78 timing"}
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -29,7 +29,7 @@ enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
 enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 
 /* ABI version (major*100 + minor) and the last error message of this thread. */
-int kw_version(void);  /* 107 */
+int kw_version(void);  /* 108 */
 const char* kw_last_error(void);
 
 /* a1 -- log-mel spectrogram.
@@ -166,7 +166,7 @@ size_t kw_self_attn_workspace(int64_t B, int64_t H, int64_t t_max);
  * kw_self_attn_step(q_len 1) without the kernel boundary (the projection and caches bitwise the same, the
  * attention output within bf16 rounding: its keys are summed in 16-slot passes): the projection's output is
  * handed to the attention in-launch as 8-byte {bf16 x 2, tag} granules while the cached K/V rows load.
- * cur_len outside [1, 256] sets the workspace error word and writes NaN.
+ * cur_len outside [1, min(256, t_max)] sets the workspace status word (kw_dec_qkv_self_status_offset) and writes NaN.
  *   x: hb [M][ldx] bf16 (the residual mirror; LayerNorm applied as kw_dec_linear's ln); W: packed [3d][d] with
  *   gamma folded (kw_pack_weight); ln_colsum / bias: [3d] f32; scale multiplies the q columns (< d);
  *   k_cache / v_cache: one layer's [M][H][t_max][64] bf16; cur_len: L on device (positions [0, L-1) cached,
@@ -241,6 +241,20 @@ int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64
                        const void* k, const void* v, int64_t S, void* out, void* workspace,
                        size_t ws_bytes, kw_stream_t stream);
 size_t kw_cross_attn_workspace(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S);
+
+/* Hand-off status of kw_dec_qkv_self / kw_dec_xq_cross / kw_cross_attn_step: the byte offset, inside the
+ * caller's workspace of that entry point (same dimensions), of an int32 STATUS word.  A launch whose in-launch
+ * hand-off poll timed out (a protocol failure, never expected) -- or, for kw_dec_qkv_self, whose cur_len was
+ * outside [1, min(256, t_max)] -- sets it nonzero and writes NaN into the rows concerned; no kernel clears it.
+ * The caller reads it after synchronizing the stream and, when it is set, rejects that work's results and
+ * zero-fills the whole workspace (a late producer may have left granules armed) before the next launch
+ * (failures surface as errors, not as tokens; kwhisper.decode raises KWError).
+ * The int32 after the status word of kw_dec_qkv_self / kw_dec_xq_cross is a FAULT-INJECTION word for tests:
+ * while it is nonzero, the next launch's first projection workgroup skips its publish and clears it, so
+ * that launch's consumers of the projection's columns [0, 16) time out and set the status word. */
+size_t kw_dec_qkv_self_status_offset(int64_t M, int64_t d);
+size_t kw_dec_xq_cross_status_offset(int64_t M, int64_t d, int64_t H, int64_t S);
+size_t kw_cross_attn_status_offset(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S);
 
 /* One greedy decoding step on f32 logits [B][V] (TF generation/utils.py:2894-2937):
  * SuppressTokens -> SuppressTokensAtBegin (when L == begin_index) -> WhisperTimeStamp (if

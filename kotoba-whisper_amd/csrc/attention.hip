@@ -1083,7 +1083,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void x
   __shared__ float red[4][64];
   __shared__ float stat[8];
   if ((int)blockIdx.x < p.n_lin) {
-    proj_publish_granules<false>(ProjArgs{p.x, p.ldx, p.M, p.d, p.d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, p.d},
+    proj_publish_granules<false>(ProjArgs{p.x, p.ldx, p.M, p.d, p.d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, p.d, p.err + 1},
                                  blockIdx.x, kv, p.qg);
     return;
   }
@@ -1783,17 +1783,23 @@ static size_t cross_partials_bytes(int64_t B, int64_t q_len, int64_t H, int64_t 
   return (size_t)(B * q_len * H) * cross_splits(S) * (HD + 2) * sizeof(float);
 }
 
-// workspace: f32 partials [rows][ns][HD+2] | arrival counters [rows] (publish_and_combine kernels) | error word,
+// workspace: f32 partials [rows][ns][HD+2] | arrival counters [rows] (publish_and_combine kernels) | status word,
+// fault-injection word (kw_dec_xq_cross's projection),
 // padded to 64 B | 8-byte granules [rows][ns][4 waves][HD+2] (cross_attn_dma_kernel, xq_cross_kernel); every region
 // zero before first use
 static size_t cross_granule_offset(int64_t B, int64_t q_len, int64_t H, int64_t S) {
-  const size_t head = cross_partials_bytes(B, q_len, H, S) + (size_t)(B * q_len * H) * sizeof(int) + sizeof(int);
+  const size_t head = cross_partials_bytes(B, q_len, H, S) + (size_t)(B * q_len * H) * sizeof(int) + 2 * sizeof(int);
   return (head + 63) & ~(size_t)63;
 }
 
 extern "C" size_t kw_cross_attn_workspace(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S) {
   (void)hd;
   return cross_granule_offset(B, q_len, H, S) + 8 * cross_partials_bytes(B, q_len, H, S);  // granules per wave
+}
+
+extern "C" size_t kw_cross_attn_status_offset(int64_t B, int64_t q_len, int64_t H, int64_t hd, int64_t S) {
+  (void)hd;
+  return cross_partials_bytes(B, q_len, H, S) + (size_t)(B * q_len * H) * sizeof(int);
 }
 
 // cross_attn_row_kernel when one round of pair workgroups covers the device -- at least one per CU, all resident
@@ -1894,6 +1900,11 @@ extern "C" size_t kw_dec_xq_cross_workspace(int64_t M, int64_t d, int64_t H, int
   return xq_gran_offset(M, H, S) + (size_t)M * (size_t)(d / 2) * sizeof(unsigned long long);
 }
 
+extern "C" size_t kw_dec_xq_cross_status_offset(int64_t M, int64_t d, int64_t H, int64_t S) {
+  (void)d;
+  return kw_cross_attn_status_offset(M, 1, H, HD, S);  // status word, then the fault-injection word
+}
+
 extern "C" int kw_dec_xq_cross_supported(int64_t M, int64_t d, int64_t H, int64_t S) {
   return xq_shape_ok(M, d, H, S) ? 1 : 0;  // (every wait is on earlier-dispatched work: no residency condition)
 }
@@ -1936,7 +1947,7 @@ extern "C" int kw_dec_xq_cross(const kw_dec_xq_cross_args* a, kw_stream_t stream
     r.H = p.H, r.d = p.d, r.S = p.S, r.chunk = p.chunk, r.ns = p.ns, r.n_lin = p.n_lin;
     r.err = p.err;
     r.out = p.out;
-    r.proj = ProjArgs{p.x, p.ldx, p.M, p.d, p.d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, p.d};
+    r.proj = ProjArgs{p.x, p.ldx, p.M, p.d, p.d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, p.d, p.err + 1};
     hipLaunchKernelGGL((cross_attn_row_kernel<true, ROW_NS>), dim3((unsigned)(p.n_lin + a->M * a->H)), dim3(256), 0,
                        (hipStream_t)stream, r);
     KW_CHECK_LAUNCH();

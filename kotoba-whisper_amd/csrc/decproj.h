@@ -26,6 +26,7 @@ struct ProjArgs {
   const float* bias;    // [N] or null
   float scale;          // multiplies columns < scale_cols (the query's head_dim^-0.5)
   int scale_cols;
+  int* fault;  // the workspace's fault-injection word (tests): nonzero -> workgroup 0 skips its publish once
 };
 
 __host__ __device__ __forceinline__ bool proj_shape_ok(int64_t M, int64_t K) {
@@ -51,6 +52,9 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
   const int n_e = min(cg * 16 + (lane & 15), a.N - 1);
   const float ebias = a.bias ? a.bias[n_e] : 0.f;
   const float ecsum = a.colsum[n_e];
+  // the fault-injection word, loaded by every workgroup (unconditionally: no phi on a loaded value) with the
+  // epilogue constants; only workgroup 0 acts on it (kw_dec_*_status_offset in include/kwhisper.h)
+  const int fault = __hip_atomic_load(a.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
@@ -139,6 +143,8 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
     rstat[lane][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + a.ln_eps);
   }
   const int n = cg * 16 + (lane & 15);
+  const bool drop = cg == 0 && fault != 0;  // test hook: this launch's consumers of columns [0, 16) time out
+  if (drop && lane == 0) __hip_atomic_store(a.fault, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
 #pragma unroll
@@ -150,7 +156,7 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
       if (n < a.scale_cols) v *= a.scale;
       const uint32_t mine = f2bf(v);
       const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, false);  // lane ^ 1
-      if ((lane & 1) == 0 && m < M && n < a.N)
+      if ((lane & 1) == 0 && m < M && n < a.N && !drop)
         __hip_atomic_store(gran + (int64_t)m * (a.N / 2) + (n >> 1), (1ull << 32) | (mine | (other << 16)),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -54,14 +54,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void q
   __shared__ uint32_t stage[QS_PAIRS][96];
   const int d = p.d, H = p.H, M = p.M;
   if ((int)blockIdx.x < p.n_lin) {
-    proj_publish_granules<true>(ProjArgs{p.x, p.ldx, M, d, 3 * d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, d},
+    proj_publish_granules<true>(ProjArgs{p.x, p.ldx, M, d, 3 * d, p.ln_eps, p.ln_colsum, p.W, p.bias, p.scale, d, p.err + 1},
                           blockIdx.x, scratch, p.gran);
     return;
   }
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ps = wave >> 1, pw = wave & 1, ptid = tid & 127;  // pair slot (2 waves each), wave within it
   const int L = *p.cur_len;  // positions [0, L - 1) cached, L - 1 new
-  const bool len_ok = L >= 1 && L <= QS_MAX_LEN;
+  const bool len_ok = L >= 1 && L <= QS_MAX_LEN && L <= p.t_max;
   const int Lc = len_ok ? L : 1;
   const int p0 = Lc - 1;
 
@@ -186,6 +186,10 @@ bool qs_shape_ok(int64_t M, int64_t d, int64_t H) {
 
 extern "C" size_t kw_dec_qkv_self_workspace(int64_t M, int64_t d) {
   return (M >= 1 && d > 0) ? qs_gran_bytes(M, d) + 64 : 0;
+}
+
+extern "C" size_t kw_dec_qkv_self_status_offset(int64_t M, int64_t d) {
+  return (M >= 1 && d > 0) ? qs_gran_bytes(M, d) : 0;  // status word, then the fault-injection word
 }
 
 extern "C" int kw_dec_qkv_self_supported(int64_t M, int64_t d, int64_t H) {

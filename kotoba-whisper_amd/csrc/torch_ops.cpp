@@ -402,6 +402,10 @@ int64_t workspace_bytes(std::string kind, std::vector<int64_t> d) {
   if (kind == "qkv_self") return (int64_t)kw_dec_qkv_self_workspace(n(0), n(1));
   if (kind == "xq_cross") return (int64_t)kw_dec_xq_cross_workspace(n(0), n(1), n(2), n(3));
   if (kind == "beam_logprobs") return (int64_t)kw_beam_logprobs_workspace(n(0));
+  // byte offsets of the hand-off status words inside those workspaces (include/kwhisper.h)
+  if (kind == "qkv_self_status") return (int64_t)kw_dec_qkv_self_status_offset(n(0), n(1));
+  if (kind == "xq_cross_status") return (int64_t)kw_dec_xq_cross_status_offset(n(0), n(1), n(2), n(3));
+  if (kind == "cross_attn_status") return (int64_t)kw_cross_attn_status_offset(n(0), n(1), n(2), n(3), n(4));
   TORCH_CHECK_VALUE(false, "kw::workspace_bytes: unknown kind ", kind);
 }
 

@@ -135,6 +135,9 @@ EXPORTS = {
     "kw_dec_xq_cross_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64]),
     "kw_dec_xq_cross_supported": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64]),
     "kw_cross_attn_pair_kernel": (ctypes.c_int, [c_i64, c_i64, ctypes.c_int]),
+    "kw_dec_qkv_self_status_offset": (ctypes.c_size_t, [c_i64, c_i64]),
+    "kw_dec_xq_cross_status_offset": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64]),
+    "kw_cross_attn_status_offset": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64, c_i64]),
     "kw_greedy_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), c_vp]),
     "kw_greedy_step_workspace": (ctypes.c_size_t, [c_i64]),
     "kw_beam_logprobs": (ctypes.c_int, [ctypes.POINTER(BeamLogprobsArgs), c_vp]),

@@ -254,6 +254,36 @@ class DecodeSession:
                                     self.T, out, ws)
 
     # ------------------------------------------------------------------------------------------
+    def status_words(self):
+        """(entry point, workspace, byte offset) of every in-launch hand-off status word this session's launches
+        can set (include/kwhisper.h kw_*_status_offset): the fused self block, the fused cross block and the
+        unfused cross-attention's combine, one per activation-buffer size."""
+        s, H = self.eng.shape, self.eng.H
+        out = []
+        if self.qs_ws is not None:
+            out.append(("kw_dec_qkv_self", self.qs_ws, ops.status_offset("qkv_self", self.R, s.d_model)))
+        if self.xc_ws is not None:
+            out.append(("kw_dec_xq_cross", self.xc_ws, ops.status_offset("xq_cross", self.R, s.d_model, H, self.T)))
+        for q, b in self._bufs.items():
+            out.append(("kw_cross_attn_step", b["ws"], ops.status_offset("cross_attn", self.B, q * self.nb, H, _HD,
+                                                                         self.T)))
+        return out
+
+    def check_handoffs(self) -> None:
+        """After the stream is synchronized: raise ``KWError`` if any launch of this session had an in-launch
+        hand-off time out (its rows were written as NaN, so its tokens are wrong).  One small device-to-host copy;
+        on failure every such workspace is zero-filled (re-armed) first, so the session stays usable."""
+        words = self.status_words()
+        if not words:
+            return
+        st = torch.stack([ws.view(torch.int32)[off // 4] for _, ws, off in words]).cpu().tolist()
+        bad = [name for (name, _, _), v in zip(words, st) if v != 0]
+        if bad:
+            for _, ws, _ in words:
+                ws.zero_()
+            raise L.KWError(f"{', '.join(sorted(set(bad)))}: an in-launch hand-off timed out (a kernel protocol "
+                            "failure); the rows it fed are NaN, so this call's tokens are invalid")
+
     def forward_logits(self, prompt: torch.Tensor) -> torch.Tensor:
         """Prefill only: logits (B, V) for the last prompt position (detect_language)."""
         P = prompt.shape[1]
@@ -279,6 +309,29 @@ class DecodeSession:
             self._run(step)
             out.append(self.logits.clone())
         return torch.stack(out, 1)
+
+    def _pinned_slots(self, n: int) -> torch.Tensor:
+        if self._pinned is None or self._pinned.numel() < n:
+            self._pinned = torch.zeros((n,), dtype=torch.int32).pin_memory()
+        return self._pinned
+
+    @staticmethod
+    def _poll(pinned, events, rep, lag, flag) -> bool:
+        """Queue a copy of the device ``flag`` (unfinished rows / beam "go") into pinned slot ``rep % (lag + 1)``
+        behind the replay just issued, then read the copy issued ``lag`` replays ago; True once that count is 0
+        (every later replay is then a no-op on device: finished rows only append pad).  The slot first gets a -1
+        sentinel, so only a count a copy actually delivered can stop the loop (r03al)."""
+        slot = rep % (lag + 1)
+        pinned[slot] = -1
+        pinned[slot: slot + 1].copy_(flag, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        events.append((ev, slot))
+        if len(events) > lag:
+            e0, s0 = events.pop(0)
+            e0.synchronize()
+            return int(pinned[s0]) == 0
+        return False
 
     def generate(self, prompt: torch.Tensor, gen, *, max_length: int, return_timestamps: bool,
                  check_every: int = 4, use_graph: bool = True, record_scores: bool = False):
@@ -381,11 +434,10 @@ class DecodeSession:
         if not use_graph:
             graph = graph_k = None
         self._graph, self._graph_key = graph, key
-        if self._pinned is None or self._pinned.numel() < check_every + 1:
-            self._pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
-        pinned = self._pinned
-        events = []
         lag = max(1, check_every // K) if graph_k is not None else check_every  # the same lag in steps
+        pinned = self._pinned_slots(lag + 1)
+        events = []
+        rep = 0  # replays issued: slot rep % (lag + 1) is distinct over the lag + 1 copies in flight
         while done < n_steps:
             if graph_k is not None and done + K <= n_steps:
                 graph_k.replay()
@@ -398,21 +450,11 @@ class DecodeSession:
                 done += 1
             if record_scores:
                 self.scores.append((self.logits.clone(), score_buf.clone()))
-            slot = done % (check_every + 1)  # (distinct over the lag + 1 copies in flight)
-            # a sentinel first: the stop test trusts only a count the copy actually delivered (r03al: a fresh
-            # pinned buffer read as 0 -- "all rows finished" -- after its event had completed but before the 4-byte
-            # D2H copy's write was visible to the host, ending the loop early); a count of 0 from any step is final
-            pinned[slot] = -1
-            pinned[slot : slot + 1].copy_(self.n_unfinished, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            events.append((ev, slot))
-            if len(events) > lag:
-                e0, s0 = events.pop(0)
-                e0.synchronize()
-                if int(pinned[s0]) == 0:
-                    break
+            if self._poll(pinned, events, rep, lag, self.n_unfinished):
+                break
+            rep += 1
         torch.cuda.synchronize(dev)
+        self.check_handoffs()
         L_now = int(self.cur_len.item())
         ids = self.ids[:, :L_now].cpu().numpy()
         return _reference_length(ids, P, gen.eos_token_id, max_length)
@@ -516,9 +558,7 @@ class DecodeSession:
         else:
             prefill()
         graph = captured("graph", one_step) if use_graph else None
-        if self._pinned is None or self._pinned.numel() < check_every + 1:
-            self._pinned = torch.zeros((check_every + 1,), dtype=torch.int32).pin_memory()
-        pinned = self._pinned
+        pinned = self._pinned_slots(check_every + 1)
         events = []
         n = 1
         while n < max_length - P + 1:
@@ -526,19 +566,11 @@ class DecodeSession:
                 graph.replay()
             else:
                 one_step()
+            if self._poll(pinned, events, n - 1, check_every, st["go"]):
+                break
             n += 1
-            slot = n % (check_every + 1)
-            pinned[slot] = -1  # sentinel: only a delivered 0 stops the loop (see generate)
-            pinned[slot: slot + 1].copy_(st["go"], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            events.append((ev, slot))
-            if len(events) > check_every:
-                e0, s0 = events.pop(0)
-                e0.synchronize()
-                if int(pinned[s0]) == 0:
-                    break
         torch.cuda.synchronize(dev)
+        self.check_handoffs()
         fin_len = st["fin_len"][:, 0].cpu().numpy()
         out = st["fin_seq"][:, 0].cpu().numpy()
         return out[:, : P + int(fin_len.max())]

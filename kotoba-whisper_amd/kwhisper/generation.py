@@ -231,9 +231,11 @@ class KWhisperForConditionalGeneration:
         batch_map = list(range(B))
         last_ids = None
         passes = 0
+        row_passes = np.zeros(B, dtype=np.int64)
         while (seek < max_frames).any():
             batch_map = [p for p in batch_map if seek[p] < max_frames[p]]
             cur = len(batch_map)
+            row_passes[batch_map] += 1
             time_offset = seek.astype(np.float64) * 0.02 / 2
             seek_num = np.minimum(max_frames - seek, nseg)
             if feats is not None:
@@ -291,7 +293,7 @@ class KWhisperForConditionalGeneration:
                 segs, off = _retrieve_segment(seq, ts_begin, int(seek_num[p]), float(time_offset[p]))
                 seek[p] += off
                 segments[p] += segs
-        self.stats = {"passes": passes}
+        self.stats = {"passes": passes, "row_passes": row_passes}
         if return_dict_in_generate and not return_timestamps:
             return {"sequences": torch.from_numpy(last_ids).to(eng.device)}
         seqs = [np.concatenate([x["tokens"] for x in segs]) if segs else np.zeros(0, np.int64) for segs in segments]

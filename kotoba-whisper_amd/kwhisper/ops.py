@@ -72,7 +72,9 @@ def _ws_bytes(kind: str, *dims) -> int:
     fn = {"dec_linear": "kw_dec_linear_workspace_bytes", "packed_weight": "kw_packed_weight_bytes",
           "self_attn": "kw_self_attn_workspace", "cross_attn": "kw_cross_attn_workspace",
           "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace",
-          "qkv_self": "kw_dec_qkv_self_workspace", "xq_cross": "kw_dec_xq_cross_workspace"}[kind]
+          "qkv_self": "kw_dec_qkv_self_workspace", "xq_cross": "kw_dec_xq_cross_workspace",
+          "qkv_self_status": "kw_dec_qkv_self_status_offset", "xq_cross_status": "kw_dec_xq_cross_status_offset",
+          "cross_attn_status": "kw_cross_attn_status_offset"}[kind]
     return int(getattr(_lib(), fn)(*dims))
 
 
@@ -428,6 +430,13 @@ class XqCrossPlan:
 
 def cross_attn_workspace_bytes(B, q_len, H, hd, S) -> int:
     return _ws_bytes("cross_attn", B, q_len, H, hd, S)
+
+
+def status_offset(kind: str, *dims) -> int:
+    """Byte offset of the int32 hand-off status word inside the workspace of ``kind`` ("qkv_self",
+    "xq_cross", "cross_attn"; the workspace's own dimensions).  The word after it (qkv_self, xq_cross) is the
+    fault-injection word (include/kwhisper.h)."""
+    return _ws_bytes(f"{kind}_status", *dims)
 
 
 def cross_attn_step(q, B, q_len, H, hd, k, v, S, out, workspace):

@@ -205,6 +205,12 @@ def decode_asr(model_outputs, *, return_timestamps, return_language=None, time_p
     return full_text, optional
 
 
+def _dist():
+    import torch.distributed as dist
+
+    return dist if dist.is_available() and dist.is_initialized() else None
+
+
 class ASRPipeline:
     """``pipeline("automatic-speech-recognition", model=<whisper>, chunk_length_s=..., batch_size=...)`` for
     the MI355X engine (TF/pipelines/automatic_speech_recognition.py, seq2seq_whisper path).
@@ -214,7 +220,7 @@ class ASRPipeline:
 
     def __init__(self, model, feature_extractor=None, tokenizer=None, *, chunk_length_s: float = 0,
                  stride_length_s=None, batch_size: int = 1, generate_kwargs: Optional[dict] = None,
-                 return_timestamps=None):
+                 return_timestamps=None, data_parallel: bool = True):
         from .feature_extraction import WhisperFeatureExtractor
 
         self.model = model
@@ -226,6 +232,9 @@ class ASRPipeline:
         self.batch_size = max(1, int(batch_size))
         self.generate_kwargs = dict(generate_kwargs or {})
         self.return_timestamps = return_timestamps
+        # with a torch.distributed process group: window batches round-robin over the ranks, one gather of the
+        # token matrices at the end, every rank returns the full result (config 5 at W GPUs)
+        self.data_parallel = bool(data_parallel)
         self.generation_config = self._pipeline_generation_config(model.generation_config)
 
     # the ASR pipeline's own generation defaults (TF/pipelines/automatic_speech_recognition.py:160-163)
@@ -371,13 +380,25 @@ class ASRPipeline:
             gk["max_new_tokens"] = mnt
         fe = self.feature_extractor
         tokens = [None] * len(flat)
-        for b0 in range(0, len(flat), bs):
+        starts = list(range(0, len(flat), bs))
+        dist = _dist() if self.data_parallel else None
+        world, rank = (dist.get_world_size(), dist.get_rank()) if dist is not None else (1, 0)
+        mine = starts[rank::world]  # data parallel: window batch j on rank j % W, no collective until the end
+        local = []
+        for b0 in mine:
             batch = flat[b0: b0 + bs]
             feats, mask = self._batch_features([c["audio"] for _, c in batch])
             out = self.model.generate(feats, attention_mask=mask, **gk)
             ids = out["sequences"] if isinstance(out, dict) else out
-            ids = ids.cpu()
-            for j in range(len(batch)):
+            local.append(ids.cpu().numpy())
+        if dist is not None:  # one exchange: every rank's window batches as generate() returned them
+            from .pseudo_label import gather_matrices
+
+            per_rank = gather_matrices(local, (len(starts) + world - 1) // world, int(self.generation_config.pad_token_id))
+            local = [per_rank[j % world][j // world] for j in range(len(starts))]
+        for b0, ids in zip(starts if dist is not None else mine, local):
+            ids = torch.from_numpy(np.ascontiguousarray(ids))
+            for j in range(ids.shape[0]):
                 tokens[b0 + j] = ids[j: j + 1]
         vocab = self._vocab()
         time_precision = fe.chunk_length / self.model.config.max_source_positions

@@ -26,7 +26,8 @@ from typing import Callable, Iterable, List, Optional, Sequence
 import numpy as np
 import torch
 
-__all__ = ["shard_batches", "gather_remainder", "pad_across_processes", "pseudo_label", "pseudo_label_multitask",
+__all__ = ["shard_batches", "gather_remainder", "pad_across_processes", "gather_matrices", "pseudo_label",
+           "pseudo_label_multitask",
            "legacy_prompt", "write_transcription_csv", "transcription_table", "write_transcription_arrow"]
 
 
@@ -86,9 +87,10 @@ def _dist():
 
 
 def pad_across_processes(ids: torch.Tensor, pad_index: int) -> torch.Tensor:
-    """Right-pad dim 1 to the widest rank's (``Accelerator.pad_across_processes(dim=1)``)."""
+    """Right-pad dim 1 to the widest rank's (``Accelerator.pad_across_processes(dim=1)``).  Whenever a process
+    group is initialised the collective runs, world size 1 included (so a one-rank RCCL run exercises it)."""
     dist = _dist()
-    if dist is None or dist.get_world_size() == 1:
+    if dist is None:
         return ids
     w = torch.tensor([ids.shape[1]], dtype=torch.int64, device=ids.device)
     dist.all_reduce(w, op=dist.ReduceOp.MAX)
@@ -102,7 +104,7 @@ def pad_across_processes(ids: torch.Tensor, pad_index: int) -> torch.Tensor:
 
 def _all_gather_rows(t: torch.Tensor) -> torch.Tensor:
     dist = _dist()
-    if dist is None or dist.get_world_size() == 1:
+    if dist is None:
         return t
     parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
     dist.all_gather(parts, t.contiguous())
@@ -132,24 +134,63 @@ def _round_path(checkpoint_dir: str, si: int) -> str:
     return os.path.join(checkpoint_dir, f"round_{si:06d}.npz")
 
 
+def _rank_round_path(checkpoint_dir: str, si: int, rank: int) -> str:
+    return os.path.join(checkpoint_dir, f"round_{si:06d}_rank{rank:03d}.npz")
+
+
+def weights_fingerprint(model) -> Optional[str]:
+    """A short digest of a few of the model's weight values (the token embedding's first rows and the decoder's
+    last layer's fc2 bias), so a resume with other weights of the same architecture is refused; None for a
+    model without an engine (test stubs)."""
+    import hashlib
+
+    eng = getattr(model, "engine", None)
+    if eng is None or getattr(eng, "tok_emb", None) is None:
+        return None
+    parts = [eng.tok_emb[:8].float().cpu().numpy().tobytes()]
+    lay = (getattr(eng, "dec_layers", None) or [None])[-1]
+    if isinstance(lay, dict) and lay.get("fc2_b") is not None:
+        parts.append(lay["fc2_b"].float().cpu().numpy().tobytes())
+    return hashlib.sha256(b"".join(parts)).hexdigest()[:16]
+
+
 def run_digest(model, **config) -> str:
     """A stable digest of what decides the labels besides the item plan: the generate kwargs, the output
-    layout options and the model (its architecture name and compute dtype).  A resume with any of them
-    changed would mix two configurations' rounds, so ``plan.json`` records it (sha256 of sorted JSON)."""
+    layout options and the model (its architecture name, compute dtype and a fingerprint of its weights).  A
+    resume with any of them changed would mix two configurations' rounds, so ``plan.json`` records it (sha256
+    of sorted JSON)."""
     import hashlib
     import json
 
     shape = getattr(getattr(model, "config", None), "shape", None)
     ident = {"model": getattr(shape, "name", None) or type(model).__name__, "dtype": str(getattr(model, "dtype", ""))}
+    fp = weights_fingerprint(model)
+    if fp is not None:
+        ident["weights"] = fp
     blob = json.dumps({"model": ident, **config}, sort_keys=True, default=repr)
     return hashlib.sha256(blob.encode()).hexdigest()
 
 
-def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict) -> List[bool]:
+def _plan_matches(stored: dict, plan: dict) -> bool:
+    """plan.json equality; a plan written before the configuration digest existed (no ``config_sha256``) is
+    accepted as legacy with a warning when everything else matches."""
+    if stored == plan:
+        return True
+    if "config_sha256" not in stored and {k: v for k, v in plan.items() if k != "config_sha256"} == stored:
+        import warnings
+
+        warnings.warn("checkpoint plan.json predates the configuration digest: resuming without checking that the "
+                      "generate kwargs / model match the rounds on disk", RuntimeWarning, stacklevel=3)
+        return True
+    return False
+
+
+def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict, rank_files: int = 0) -> List[bool]:
     """Which gathered rounds already have a checkpoint file, as rank 0 sees it (broadcast: every rank skips
     the same rounds, so the per-round collectives stay matched).  The directory's ``plan.json`` (items,
     batch size, world size, and the digest of the generate kwargs / output layout / model) must match this
-    run's: the rounds of another plan hold other items or other labels."""
+    run's: the rounds of another plan hold other items or other labels.  ``rank_files`` = W (deferred gather):
+    a round counts as done when every rank's own file of it exists."""
     if not checkpoint_dir or n_steps == 0:
         return [False] * n_steps
     import json
@@ -161,14 +202,18 @@ def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict
         meta = os.path.join(checkpoint_dir, "plan.json")
         if os.path.exists(meta):
             with open(meta) as f:
-                mask[0] = int(json.load(f) != plan)
+                mask[0] = int(not _plan_matches(json.load(f), plan))
         else:
             with open(meta + ".tmp", "w") as f:
                 json.dump(plan, f)
             os.replace(meta + ".tmp", meta)
         if not int(mask[0]):
             for si in range(n_steps):
-                mask[si + 1] = int(os.path.exists(_round_path(checkpoint_dir, si)))
+                if rank_files:
+                    ok = all(os.path.exists(_rank_round_path(checkpoint_dir, si, r)) for r in range(rank_files))
+                else:
+                    ok = os.path.exists(_round_path(checkpoint_dir, si))
+                mask[si + 1] = int(ok)
     if dist is not None and dist.get_world_size() > 1:
         dist.broadcast(mask, 0)
     m = mask.cpu().tolist()
@@ -177,16 +222,16 @@ def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict
     return [bool(x) for x in m[1:]]
 
 
-def _save_round(checkpoint_dir: str, si: int, fid: List[int], mats: List[np.ndarray]) -> None:
-    path = _round_path(checkpoint_dir, si)
+def _save_round(checkpoint_dir: str, si: int, fid: List[int], mats: List[np.ndarray], path: Optional[str] = None) -> None:
+    path = path or _round_path(checkpoint_dir, si)
     tmp = f"{path}.{os.getpid()}.tmp"
     with open(tmp, "wb") as f:
         np.savez(f, fid=np.asarray(fid, dtype=np.int64), **{f"c{c}": m for c, m in enumerate(mats)})
     os.replace(tmp, path)  # atomic: a restart sees the whole round or none of it
 
 
-def _load_round(checkpoint_dir: str, si: int):
-    with np.load(_round_path(checkpoint_dir, si), allow_pickle=False) as z:
+def _load_round(checkpoint_dir: str, si: int, path: Optional[str] = None):
+    with np.load(path or _round_path(checkpoint_dir, si), allow_pickle=False) as z:
         n_cols = sum(1 for k in z.files if k.startswith("c"))
         return z["fid"].tolist(), [z[f"c{c}"] for c in range(n_cols)]
 
@@ -253,10 +298,119 @@ def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device,
     return eval_ids, cols or []
 
 
+def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
+                         checkpoint_dir=None, digest=None):
+    """``_label_loop`` with the per-round collectives deferred to ONE exchange at the end (``gather="end"``).
+
+    The reference pads and gathers after every batch (run_pseudo_labelling.py:339-341), so every round waits
+    for the slowest rank's batch; with timestamps a batch's cost depends on its seek passes, so that lock step
+    loses throughput at W > 1.  Here each rank decodes its whole shard (accelerate's plan, ``shard_batches``)
+    without a collective, keeps its per-batch matrices and widths, and at the end one all-reduce(MAX) of the
+    width and two all-gathers (per-round widths, the padded token rows) rebuild exactly the rounds the
+    per-batch gather would have produced: each round's rows padded to that round's widest rank, the wrapped
+    duplicates of the final round dropped, file ids from the (deterministic) shard plan of every rank.
+    Resume: each rank checkpoints its own batches (``round_<step>_rank<r>.npz``); a round counts as done when
+    every rank's file of it exists (rank 0's view, broadcast once)."""
+    dist = _dist()
+    world = dist.get_world_size() if dist else 1
+    rank = dist.get_rank() if dist else 0
+    plans = [shard_batches(n_items, batch_size, world, r) for r in range(world)]
+    steps = plans[rank]
+    n_steps = len(steps)
+    rem = gather_remainder(n_items, batch_size, world)
+    if checkpoint_dir and rank == 0:
+        os.makedirs(checkpoint_dir, exist_ok=True)
+    dev = comm_device if comm_device is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if dist is not None and dist.get_backend() == "nccl"
+        else torch.device("cpu"))
+    done = _done_rounds(checkpoint_dir, n_steps, dev,
+                        {"n_items": int(n_items), "batch_size": int(batch_size), "world_size": int(world),
+                         "config_sha256": digest, "gather": "end"}, rank_files=world)
+    local: List[List[np.ndarray]] = []  # [step][column] -> (batch_size, width) int64
+    for si, idx in enumerate(steps):
+        path = _rank_round_path(checkpoint_dir, si, rank) if checkpoint_dir else None
+        if done[si]:
+            _, mats = _load_round(checkpoint_dir, si, path)
+        else:
+            mats = [o.cpu().numpy().astype(np.int64) for o in decode(features(idx))]
+            if checkpoint_dir:
+                _save_round(checkpoint_dir, si, list(idx), mats, path)
+        if local and len(mats) != len(local[0]):
+            raise ValueError(f"step {si} produced {len(mats)} output columns, earlier steps {len(local[0])}")
+        local.append(mats)
+        if on_step is not None:
+            on_step(si, n_steps)
+    n_cols = len(local[0]) if local else 0
+    if dist is not None:  # every rank runs the same number of steps (even_batches): agree on the column count
+        t = torch.tensor([n_cols], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        n_cols = int(t.item())
+    eval_ids: List[int] = []
+    for si in range(n_steps):
+        fid = [i for r in range(world) for i in plans[r][si]]
+        eval_ids.extend(fid[:rem] if si == n_steps - 1 and rem > 0 else fid)
+    cols: List[List[np.ndarray]] = []
+    for c in range(n_cols):
+        per_rank = gather_matrices([m[c] for m in local], n_steps, pad_token_id, dev)
+        out: List[np.ndarray] = []
+        for si in range(n_steps):
+            w = max(per_rank[r][si].shape[1] for r in range(world))  # the round's common width
+            rnd = []
+            for r in range(world):
+                m = per_rank[r][si]
+                pm = np.full((m.shape[0], w), pad_token_id, dtype=np.int64)
+                pm[:, : m.shape[1]] = m
+                rnd.append(pm)
+            mat = np.concatenate(rnd, 0)
+            if si == n_steps - 1 and rem > 0:
+                mat = mat[:rem]
+            out.extend(mat)
+        cols.append(out)
+    return eval_ids, cols
+
+
+def gather_matrices(mats: Sequence[np.ndarray], n_slots: int, pad: int, device=None) -> List[List[np.ndarray]]:
+    """Every rank's list of int64 matrices, on every rank, exactly as each rank held them (shapes included): one
+    all_reduce(MAX) of the largest shape, then all_gathers of the shapes and of the matrices padded to it.
+    ``n_slots`` >= the longest list over ranks (unused slots travel as padding).  Without a process group: [mats]."""
+    dist = _dist()
+    mats = [np.asarray(m, dtype=np.int64).reshape(np.shape(m)[0], -1) for m in mats]
+    if dist is None:
+        return [list(mats)]
+    if len(mats) > n_slots:
+        raise ValueError(f"{len(mats)} matrices for {n_slots} slots")
+    world = dist.get_world_size()
+    dev = device if device is not None else (
+        torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu"))
+    big = torch.tensor([max([m.shape[0] for m in mats], default=0), max([m.shape[1] for m in mats], default=0)],
+                       dtype=torch.int64, device=dev)
+    dist.all_reduce(big, op=dist.ReduceOp.MAX)
+    R, T = max(int(big[0]), 1), max(int(big[1]), 1)
+    shapes = np.full((n_slots, 2), -1, dtype=np.int64)  # -1: unused slot
+    buf = np.full((n_slots, R, T), pad, dtype=np.int64)
+    for i, m in enumerate(mats):
+        shapes[i] = m.shape
+        buf[i, : m.shape[0], : m.shape[1]] = m
+    g_s = _all_gather_rows(torch.from_numpy(shapes).to(dev)).view(world, n_slots, 2).cpu().numpy()
+    g_b = _all_gather_rows(torch.from_numpy(buf).to(dev)).view(world, n_slots, R, T).cpu().numpy()
+    return [[g_b[r, i, : g_s[r, i, 0], : g_s[r, i, 1]] for i in range(n_slots) if g_s[r, i, 0] >= 0]
+            for r in range(world)]
+
+
+_GATHER = {"round": _label_loop, "end": _label_loop_deferred}
+
+
+def _loop(gather):
+    try:
+        return _GATHER[gather]
+    except KeyError:
+        raise ValueError(f"gather must be 'round' (the reference's per-batch gather) or 'end', got {gather!r}") from None
+
+
 def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *, batch_size: int,
                  pad_token_id: int, gen_kwargs: Optional[dict] = None, comm_device=None,
                  on_step: Optional[Callable[[int, int], None]] = None, legacy_prompt_in_output: bool = False,
-                 checkpoint_dir: Optional[str] = None):
+                 checkpoint_dir: Optional[str] = None, gather: str = "round"):
     """Transcribe items 0..n_items-1 data-parallel; returns (item_indices, predictions) in dataset order
     on every rank (``run_pseudo_labelling.py:333-344``).
 
@@ -268,8 +422,11 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
     ``<|endoftext|>`` (the eos id, 50257), not ``generation_config.pad_token_id`` (50256), which only pads
     rows inside one generate() output.
     ``legacy_prompt_in_output`` prepends ``legacy_prompt(...)`` to every row (needs ``language``).
-    ``checkpoint_dir``: checkpoint every gathered round there and skip rounds already written (resume)."""
+    ``checkpoint_dir``: checkpoint every gathered round there and skip rounds already written (resume).
+    ``gather``: "round" pads and gathers after every batch as the reference does; "end" defers every collective
+    to one exchange after the rank's last batch (``_label_loop_deferred``: the same predictions, no lock step)."""
     gen_kwargs = dict(gen_kwargs or {})
+    loop = _loop(gather)
     prompt = None
     if legacy_prompt_in_output:
         if not gen_kwargs.get("language"):
@@ -283,20 +440,22 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
 
     digest = run_digest(model, gen_kwargs=gen_kwargs, pad_token_id=int(pad_token_id),
                         legacy_prompt_in_output=bool(legacy_prompt_in_output)) if checkpoint_dir else None
-    eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                                 checkpoint_dir, digest)
+    eval_ids, cols = loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
+                          checkpoint_dir, digest)
     return eval_ids, (cols[0] if cols else [])
 
 
 def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *,
                            batch_size: int, text_lang_task: Sequence[tuple], pad_token_id: int,
                            gen_kwargs: Optional[dict] = None, comm_device=None,
-                           on_step: Optional[Callable[[int, int], None]] = None, checkpoint_dir: Optional[str] = None):
+                           on_step: Optional[Callable[[int, int], None]] = None, checkpoint_dir: Optional[str] = None,
+                           gather: str = "round"):
     """``run_pseudo_labelling_v3.py:299-321``: every batch is decoded once per (text, lang, task) triple.
     Returns (item_indices, {text: predictions}) in dataset order; ``whisper_<text>`` is the column the
     reference adds (:322-323).  The encoder and cross-K/V run once per batch (``generate_multitask``) when
     the model offers it, so each extra task costs only its decode loop."""
     gen_kwargs = dict(gen_kwargs or {})
+    loop = _loop(gather)
     tasks = [(lang, task) for _, lang, task in text_lang_task]
 
     def decode(feats):
@@ -306,8 +465,8 @@ def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tens
 
     digest = run_digest(model, gen_kwargs=gen_kwargs, pad_token_id=int(pad_token_id),
                         text_lang_task=[list(t) for t in text_lang_task]) if checkpoint_dir else None
-    eval_ids, cols = _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                                 checkpoint_dir, digest)
+    eval_ids, cols = loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
+                          checkpoint_dir, digest)
     if not cols:
         cols = [[] for _ in text_lang_task]
     return eval_ids, {t[0]: c for t, c in zip(text_lang_task, cols)}

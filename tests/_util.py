@@ -75,8 +75,11 @@ def long_audio(kind, seed, seconds):
 
 
 def clip_audio(spec):
-    """"kind:seed:seconds" -> tools/make_fixtures.py pipeline_audio / long_audio."""
+    """"kind:seed:seconds" -> tools/make_fixtures.py pipeline_audio / long_audio ("reazon": clip ``seed`` of the
+    config-4/5 stand-in, kwhisper.synthetic.reazon_audio)."""
     kind, seed, sec = str(spec).split(":")
+    if kind == "reazon":
+        return S.reazon_audio(int(seed), float(sec))
     return long_audio(kind, int(seed), float(sec))
 
 

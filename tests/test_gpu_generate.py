@@ -429,3 +429,28 @@ def test_steps_per_replay_tokens_identical(tiny16, ts, eos):
     finally:
         eng.steps_per_replay = 2
     assert torch.equal(out[1], out[2]) and torch.equal(out[1], out[3])
+
+
+@pytest.mark.parametrize("block", ["kw_dec_qkv_self", "kw_dec_xq_cross"])
+def test_handoff_timeout_raises(gold, tiny16, block):
+    """A fused decode block whose in-launch hand-off times out must fail the call, not return tokens (VERDICT r3
+    item 3; SURVEY §8b "HIP errors -> RuntimeError"): the workspace's fault-injection word makes ONE launch's
+    first projection workgroup skip its publish, that launch's consumers time out (NaN rows + status word), and
+    generate() raises KWError after its final synchronize.  The session re-arms its workspaces, so the next
+    call returns the tokens of an undisturbed run."""
+    from kwhisper._lib import KWError
+
+    g = gold("tiny_fp32")
+    feats = torch.from_numpy(oracle_features(TINY, g["cases"][:2])).cuda()
+    kw = dict(language="ja", task="transcribe", max_length=24)
+    want = tiny16.generate(feats, **kw).cpu().numpy()
+    sess = tiny16._session(2)
+    words = {name: (ws, off) for name, ws, off in sess.status_words()}
+    assert {"kw_dec_qkv_self", "kw_dec_xq_cross"} <= set(words)  # the greedy bf16 step runs both fused blocks
+    ws, off = words[block]
+    ws.view(torch.int32)[off // 4 + 1] = 1  # arm the fault-injection word
+    with pytest.raises(KWError, match=block):
+        tiny16.generate(feats, **kw)
+    assert int(ws.view(torch.int32)[off // 4 + 1]) == 0  # consumed by exactly one launch
+    assert all(int(w.view(torch.int32)[o // 4]) == 0 for _, w, o in sess.status_words())  # re-armed
+    np.testing.assert_array_equal(tiny16.generate(feats, **kw).cpu().numpy(), want)

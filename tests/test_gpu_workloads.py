@@ -310,6 +310,74 @@ def test_config5_pipeline_kotoba_bf16_runs(gold):
     _free()
 
 
+def test_config5_b64_pipeline_fp32_bitexact_bf16_rescored(gold, kotoba32):
+    """Config 5 at its BASELINE batch (bs = 64 windows x 5 beams = 320 rows; run_short_form_eval.py:110-117,
+    184-191, chunk_length_s 15, timestamps): 22 of tools/bench_configs.py's 30 s clips -> 66
+    windows -> window batches of 64 and 2 through ASRPipeline, against the real transformers fp32 pipeline
+    (tests/golden/pipeline_kotoba_v2_b64_fp32.npz).  The fp32 engine: every window batch's tokens and the merged
+    text bit-exact.  The bf16 engine on the 64-window batch: each window's chosen hypothesis, rescored by the fp32
+    engine, is as good as the fp32 beam's choice within the bf16 scoring noise of the two hypotheses (HF beam
+    score: sum of log-probs / length, utils.py:3182)."""
+    from kwhisper.pipeline import ASRPipeline
+
+    g = gold("pipeline_kotoba_v2_b64_fp32")
+    gk = json.loads(str(g["generate_kwargs"]))
+    gen = generation_constants(KOTOBA_V2)
+    pipe = ASRPipeline(kotoba32, feature_extractor=OracleFeatureExtractor(KOTOBA_V2.num_mel_bins), tokenizer=StubTok(gen),
+                       chunk_length_s=float(g["chunk_length_s"]), batch_size=int(g["batch_size"]), generate_kwargs=gk)
+    calls = []
+    orig = kotoba32.generate
+
+    def rec(feats, **kw):
+        out = orig(feats, **kw)
+        calls.append((feats, kw, (out["sequences"] if isinstance(out, dict) else out).cpu().numpy()))
+        return out
+
+    kotoba32.generate = rec
+    try:
+        got = pipe([{"array": clip_audio(c), "sampling_rate": 16000} for c in g["clips"]], return_timestamps=True)
+    finally:
+        del kotoba32.generate
+    assert len(calls) == int(g["ts1_n_calls"]) == 2 and calls[0][0].shape[0] == 64
+    for i, (_, _, toks) in enumerate(calls):
+        np.testing.assert_array_equal(toks, g[f"ts1_call{i}"], err_msg=f"window batch {i}")
+    assert jsonable(got) == json.loads(str(g["ts1_result"]))
+    # the bf16 engine on the same 64-window batch (320 beam rows)
+    feats, kw, t32 = calls[0]
+    m16 = _model(KOTOBA_V2, torch.bfloat16)
+    t16 = m16.generate(feats, **kw).cpu().numpy()
+    prompt = [gen.decoder_start_token_id, gen.lang_to_id["<|ja|>"], gen.task_to_id["transcribe"]]  # timestamps
+    P, max_new = len(prompt), int(gk["max_length"])
+    e32 = kotoba32.engine.encode(feats).view(64, 1500, -1)
+    e16 = m16.engine.encode(feats).view(64, 1500, -1)
+
+    def hyp(row):
+        r = [int(x) for x in row]
+        while r and r[-1] == gen.pad_token_id:
+            r.pop()
+        return prompt + r + ([gen.eos_token_id] if len(r) < max_new else [])
+
+    same, worst = 0, 0.0
+    for b in range(64):
+        h16, h32 = hyp(t16[b]), hyp(t32[b])
+        if h16 == h32:
+            same += 1
+            continue
+        s = {}
+        for name, h in (("h16", h16), ("h32", h32)):
+            lp32 = _tf_logprobs(kotoba32.engine, e32[b:b + 1].reshape(1500, -1), h, P)
+            lp16 = _tf_logprobs(m16.engine, e16[b:b + 1].reshape(1500, -1), h, P)
+            s[name] = (lp32.sum() / len(lp32), lp16.sum() / len(lp16))
+        tol = abs(s["h16"][1] - s["h16"][0]) + abs(s["h32"][1] - s["h32"][0]) + 1e-4
+        worst = max(worst, s["h32"][0] - s["h16"][0])
+        assert s["h16"][0] >= s["h32"][0] - tol, (b, s, tol)
+    print(f"\nconfig5 b64: fp32 pipeline bit-exact (2 window batches, 22 clips' merged text); bf16 at R = 320: "
+          f"{same}/64 windows chose the fp32 hypothesis, the others within tolerance (largest fp32-score deficit "
+          f"{worst:.5f})")
+    del m16
+    _free()
+
+
 # ---------------------------------------------------------------------------------------------------------
 # tiny pipeline fixtures (the reference's own pipeline; no transformers on the GPU box)
 

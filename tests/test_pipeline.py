@@ -8,6 +8,8 @@
   chunk outputs with timestamps, strides, language tokens and prompts.
 The GPU end-to-end test lives in test_gpu_generate.py.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -189,3 +191,93 @@ def test_pipeline_generation_defaults_match_transformers():
         got = ASRPipeline._pipeline_generation_config(ours)
         assert got.num_beams == p.generation_config.num_beams == 5
         assert got.pipeline_max_new_tokens == p.generation_config.max_new_tokens, max_length
+
+
+# ---- data-parallel pipeline (config 5 at W GPUs) -----------------------------------------
+class _StubFE:
+    """Feature-extractor stand-in (CPU): one 2-value 'frame' per window -- its sample count and a checksum."""
+
+    sampling_rate, n_samples, padding_value, chunk_length, hop_length = 16000, 480000, 0.0, 30, 160
+    device = "cpu"
+
+    def __call__(self, audios, sampling_rate=None, return_attention_mask=None, **kw):
+        import torch
+
+        f = torch.tensor([[[len(a), float(np.round(np.abs(a).sum() * 1e3))]] for a in audios], dtype=torch.float32)
+        return {"input_features": f, "attention_mask": torch.ones((len(audios), 1), dtype=torch.int32)}
+
+
+class _StubASRModel:
+    """generate(): a deterministic token row per window (1-4 tokens), right-padded to the batch's longest."""
+
+    class config:  # noqa: N801
+        max_source_positions, num_mel_bins = 1500, 80
+
+    device = "cpu"
+
+    def __init__(self):
+        self.generation_config = G.copy()
+        self.calls = 0
+
+    def generate(self, feats, attention_mask=None, **kw):
+        import torch
+
+        self.calls += 1
+        keys = [int(f[0, 0]) * 7 + int(f[0, 1]) for f in feats]
+        rows = [[100 + (k % 50) + j for j in range(1 + k % 4)] for k in keys]
+        T = max(len(r) for r in rows)
+        out = torch.full((len(rows), T), G.pad_token_id, dtype=torch.int64)
+        for i, r in enumerate(rows):
+            out[i, : len(r)] = torch.tensor(r)
+        return out
+
+
+_DP_CLIPS = [7.0, 40.0, 22.0, 15.0, 31.0, 3.5]
+
+
+def _dp_clips():
+    rng = np.random.default_rng(5)
+    return [{"array": (rng.random(int(s * 16000)) - 0.5).astype(np.float32), "sampling_rate": 16000} for s in _DP_CLIPS]
+
+
+def _dp_pipe_worker(rank, world, port, out_dir):
+    import json
+
+    import torch.distributed as dist
+
+    from kwhisper.pipeline import ASRPipeline
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        m = _StubASRModel()
+        got = ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2)(_dp_clips())
+        with open(os.path.join(out_dir, f"p{rank}.json"), "w") as f:
+            json.dump({"res": got, "calls": m.calls}, f, default=lambda x: x.tolist() if hasattr(x, "tolist") else x)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_pipeline_data_parallel_gloo_matches_single_process(tmp_path, world):
+    """ASRPipeline under a process group: window batch j runs on rank j % W, one gather at the end, every rank's
+    merged output equals the single-process run's, and each rank decoded only its share of the batches."""
+    import json
+    import socket
+
+    import torch.multiprocessing as mp
+
+    from kwhisper.pipeline import ASRPipeline
+
+    m1 = _StubASRModel()
+    want = json.loads(json.dumps(ASRPipeline(m1, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2)(_dp_clips()),
+                                 default=lambda x: x.tolist() if hasattr(x, "tolist") else x))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_dp_pipe_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    calls = []
+    for r in range(world):
+        z = json.load(open(tmp_path / f"p{r}.json"))
+        assert z["res"] == want
+        calls.append(z["calls"])
+    assert sum(calls) == m1.calls and max(calls) - min(calls) <= 1

@@ -317,3 +317,83 @@ def test_resume_gloo_world2(tmp_path):
         np.testing.assert_array_equal(a["preds"], b["preds"])
         # the second run decoded round 2 only: items 8-9 on rank 0, 10-11 on rank 1
         assert b["decoded"].tolist() == [[8, 9], [10, 11]][r]
+
+
+# ---- deferred gather (gather="end": one exchange after the last batch) --------------------
+def _deferred_worker(rank, world, port, n, bs, out_dir, ck):
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        m = _CountingModel()
+        ids_r, preds_r = pseudo_label(_StubModel(), _features, n, batch_size=bs, pad_token_id=PAD)
+        ids_e, preds_e = pseudo_label(m, _features, n, batch_size=bs, pad_token_id=PAD, gather="end",
+                                      checkpoint_dir=ck or None)
+        np.savez(os.path.join(out_dir, f"d{rank}.npz"), ids_r=np.array(ids_r), ids_e=np.array(ids_e),
+                 pr=np.array([p.tolist() + [-1] * (16 - len(p)) for p in preds_r]),
+                 pe=np.array([p.tolist() + [-1] * (16 - len(p)) for p in preds_e]),
+                 decoded=np.array([i for b in m.batches for i in b] or [-1]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,bs,world", [(13, 4, 2), (16, 4, 2), (3, 4, 2), (23, 3, 3), (0, 4, 2)])
+def test_deferred_gather_equals_per_round_gather(tmp_path, n, bs, world):
+    """gather="end" returns, on every rank, exactly what the reference's per-batch pad + gather returns: the same
+    items in dataset order, each row padded to its round's widest rank (ragged widths, wrapped final round)."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_deferred_worker, args=(world, _free_port(), n, bs, str(tmp_path), ""), nprocs=world, join=True)
+    ids1, preds1 = pseudo_label(_StubModel(), _features, n, batch_size=bs, pad_token_id=PAD, gather="end")
+    assert ids1 == list(range(n))
+    for r in range(world):
+        z = np.load(tmp_path / f"d{r}.npz")
+        if n == 0:
+            continue
+        assert z["ids_e"].tolist() == z["ids_r"].tolist() == list(range(n))
+        np.testing.assert_array_equal(z["pe"], z["pr"])
+
+
+def test_deferred_gather_single_process_equals_round():
+    a = pseudo_label(_StubModel(), _features, 23, batch_size=4, pad_token_id=PAD)
+    b = pseudo_label(_StubModel(), _features, 23, batch_size=4, pad_token_id=PAD, gather="end")
+    _same(a, b)
+    with pytest.raises(ValueError, match="gather"):
+        pseudo_label(_StubModel(), _features, 3, batch_size=4, pad_token_id=PAD, gather="never")
+
+
+def test_deferred_gather_resume_gloo_world2(tmp_path):
+    """Deferred mode checkpoints each rank's batches itself; after one rank's file of round 2 is lost, the rerun
+    decodes round 2 on both ranks (a round is done only when every rank's file of it exists) and nothing else."""
+    import torch.multiprocessing as mp
+
+    n, bs = 13, 2
+    ck = str(tmp_path / "ck")
+    mp.spawn(_deferred_worker, args=(2, _free_port(), n, bs, str(tmp_path), ck), nprocs=2, join=True)
+    a = [np.load(tmp_path / f"d{r}.npz") for r in range(2)]
+    assert sorted(f for f in os.listdir(ck) if f.endswith(".npz")) == [
+        f"round_{s:06d}_rank{r:03d}.npz" for s in range(4) for r in range(2)]
+    os.remove(os.path.join(ck, "round_000002_rank001.npz"))
+    mp.spawn(_deferred_worker, args=(2, _free_port(), n, bs, str(tmp_path), ck), nprocs=2, join=True)
+    for r in range(2):
+        b = np.load(tmp_path / f"d{r}.npz")
+        np.testing.assert_array_equal(a[r]["pe"], b["pe"])
+        assert b["ids_e"].tolist() == list(range(n))
+        assert b["decoded"].tolist() == [[8, 9], [10, 11]][r]
+
+
+def test_resume_accepts_legacy_plan_without_digest(tmp_path):
+    """A checkpoint directory written before plan.json carried config_sha256 resumes (with a warning) instead of
+    being refused as another plan."""
+    import json
+
+    ck = tmp_path / "ck"
+    ref = pseudo_label(_StubModel(), _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=str(ck))
+    plan = json.loads((ck / "plan.json").read_text())
+    plan.pop("config_sha256")
+    (ck / "plan.json").write_text(json.dumps(plan))
+    m = _CountingModel()
+    with pytest.warns(RuntimeWarning, match="predates"):
+        got = pseudo_label(m, _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=str(ck))
+    _same(got, ref)
+    assert m.batches == []

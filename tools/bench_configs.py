@@ -15,6 +15,7 @@ Random-init weights of each architecture (no checkpoints offline); one JSON line
     python tools/bench_configs.py --config 4 [--n-clips 1768]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_configs.py --config 4
     python tools/bench_configs.py --config 5 [--clips 64]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 tools/bench_configs.py --config 5
 """
 from __future__ import annotations
 
@@ -81,24 +82,51 @@ def config4(a, world, rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    stamps, passes = [], []
+
+    def on_step(si, total):  # after each batch's tokens reached the host (and, gather="round", the gather)
+        stamps.append(time.perf_counter())
+        passes.append(int(model.stats.get("passes", 0)))
+
     t0 = time.perf_counter()
-    ids, preds = pseudo_label(model, features, n, batch_size=a.batch, gen_kwargs=gen_kw,
-                              pad_token_id=model.generation_config.eos_token_id)  # tokenizer pad = <|endoftext|>
+    ids, preds = pseudo_label(model, features, n, batch_size=a.batch, gen_kwargs=gen_kw, gather=a.gather,
+                              pad_token_id=model.generation_config.eos_token_id,  # tokenizer pad = <|endoftext|>
+                              on_step=on_step)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
     assert ids == list(range(n))
+    batch_s = np.diff([t0] + stamps)
     return {"metric": "audio-seconds/sec pseudo-labelling (real durations)", "value": float(durs.sum()) / dt,
             "unit": "audio-s/s", "padded_30s_value": n * 30.0 / dt, "n_gpus": world, "clips": n,
             "audio_seconds": float(durs.sum()), "seconds": dt, "higher_is_better": True, "scaling": "strong",
             "dtype": "bf16", "data": "synthetic (ReazonSpeech-tiny duration statistics, noise audio, random weights)",
             "config": {"workload": "config 4: run_pseudo_labelling.py loop, whisper-large-v3, timestamps, greedy",
                        "per_gpu_batch": a.batch, "max_length": a.max_length, "parallelism": f"dp{world}",
-                       "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))}}
+                       "gather": a.gather, "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))},
+            "batch_seconds": [round(float(x), 5) for x in batch_s], "batch_seek_passes": passes,
+            "dp_projection": dp_projection(batch_s) if world == 1 else None}
 
 
-def config5(a, dev):
+def dp_projection(batch_s, worlds=(2, 4, 8)):
+    """Projected data-parallel efficiency at W ranks from W = 1 per-batch times.  Global batch
+    i runs on rank i % W (accelerate's shard plan; the wrapped duplicates of the last round are real work).
+    Lock step (the reference's per-batch gather, gather="round"): every round waits for its slowest batch,
+    efficiency = sum over rounds of the mean batch time / sum of the max.  Deferred (gather="end"): ranks run
+    free until one exchange, efficiency = (total / W) / the busiest rank's sum."""
+    t = np.asarray(batch_s, dtype=np.float64)
+    out = {}
+    for W in worlds:
+        n_rounds = -(-len(t) // W)
+        tt = np.concatenate([t, t[: n_rounds * W - len(t)]]) if n_rounds * W > len(t) else t  # wrap-around
+        r = tt.reshape(n_rounds, W)
+        out[f"w{W}"] = {"lockstep": round(float(r.mean(1).sum() / r.max(1).sum()), 4),
+                        "deferred": round(float(r.sum() / W / r.sum(0).max()), 4)}
+    return out
+
+
+def config5(a, world, rank, dev):
     from kwhisper.config import PRESETS
     from kwhisper.generation import KWhisperForConditionalGeneration
     from kwhisper.pipeline import ASRPipeline
@@ -108,21 +136,33 @@ def config5(a, dev):
     sd = synthetic_state_dict_torch(shape, seed=0, device=dev)
     model = KWhisperForConditionalGeneration.from_state_dict(shape, sd, dtype=torch.bfloat16, device=dev)
     del sd
+    # W > 1: the pipeline's window batches go round-robin over the ranks (ASRPipeline.data_parallel), one
+    # gather of the token matrices at the end; every rank merges the full result
     pipe = ASRPipeline(model, chunk_length_s=15, batch_size=a.batch,
                        generate_kwargs=dict(language="ja", task="transcribe", num_beams=5, max_length=a.max_length))
     clips = [{"array": clip_audio(i, 30.0), "sampling_rate": SR} for i in range(a.clips)]
-    pipe(clips[: max(1, a.batch // 3)], return_timestamps=True)  # warm-up
+    warm = ASRPipeline(model, chunk_length_s=15, batch_size=a.batch, data_parallel=False,
+                       generate_kwargs=dict(language="ja", task="transcribe", num_beams=5, max_length=a.max_length))
+    warm(clips[: max(1, a.batch // 3)], return_timestamps=True)  # warm-up (graph capture), no collective
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     t0 = time.perf_counter()
     out = pipe(clips, return_timestamps=True)
     torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
     dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
     return {"metric": "audio-seconds/sec ASR pipeline (chunk 15 s, beam 5, timestamps)",
-            "value": a.clips * 30.0 / dt, "unit": "audio-s/s", "n_gpus": 1, "clips": a.clips, "seconds": dt,
-            "higher_is_better": True, "dtype": "bf16",
+            "value": a.clips * 30.0 / dt, "unit": "audio-s/s", "n_gpus": world, "clips": a.clips, "seconds": dt,
+            "higher_is_better": True, "dtype": "bf16", "scaling": "strong",
             "data": "synthetic (run_speed_eval.py noise audio, random-init kotoba-whisper-v2.0 layout)",
             "config": {"workload": "config 5: kotoba-v2.0 (32 enc / 2 dec), beam 5 + timestamps, chunk_length_s 15",
-                       "batch_windows": a.batch, "max_length": a.max_length,
+                       "batch_windows": a.batch, "max_length": a.max_length, "parallelism": f"dp{world}",
                        "tokens_per_clip_mean": float(np.mean([len(o["tokens"]) for o in out]))}}
 
 
@@ -133,6 +173,8 @@ def main():
     ap.add_argument("--clips", type=int, default=64)
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--max-length", type=int, default=128)
+    ap.add_argument("--gather", choices=("round", "end"), default="end",
+                    help="config 4: the reference's per-batch gather (round) or one exchange at the end")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -146,7 +188,7 @@ def main():
         res = config4(a, world, rank, dev)
     else:
         a.batch = a.batch or 64
-        res = config5(a, dev)
+        res = config5(a, world, rank, dev)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -1,0 +1,71 @@
+#!/usr/bin/env python
+"""Which config-4 stand-in clips take more than one seek pass at ``max_length`` 128 (GPU, fp32 parity mode).
+
+The fp32 engine is bit-exact with transformers' fp32 generate (tests/test_gpu_workloads.py), so the clips it
+decodes in >= 2 passes of the timestamp seek loop (generation_whisper.py:785-903, the cumulative max_length growth
+:1935-1940) are the ones transformers also re-encodes.  tools/make_fixtures.py --only large_c4 then builds the
+config-4 fixture over a 32-clip batch that contains such clips.
+
+    python tools/find_multipass.py --n-clips 640 --out gpurun_out/multipass.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "kotoba-whisper_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-clips", type=int, default=640)
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--out", default="gpurun_out/multipass.json")
+    a = ap.parse_args()
+    from kwhisper.config import LARGE_V3, generation_constants
+    from kwhisper.feature_extraction import WhisperFeatureExtractor
+    from kwhisper.generation import KWhisperForConditionalGeneration
+    from kwhisper.synthetic import reazon_audio, reazon_durations, synthetic_state_dict_torch
+
+    dev = torch.device("cuda", 0)
+    sd = synthetic_state_dict_torch(LARGE_V3, seed=0, device=dev)
+    model = KWhisperForConditionalGeneration.from_state_dict(LARGE_V3, sd, dtype=getattr(torch, a.dtype), device=dev,
+                                                             generation_config=generation_constants(LARGE_V3))
+    del sd
+    fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins, device=dev)
+    durs = reazon_durations()[: a.n_clips]
+    passes, ntok = [], []
+    t0 = time.time()
+    for b0 in range(0, len(durs), a.batch):
+        idx = list(range(b0, min(b0 + a.batch, len(durs))))
+        audio = np.zeros((len(idx), 480000), np.float32)
+        for j, i in enumerate(idx):
+            c = reazon_audio(i, float(durs[i]))
+            audio[j, : len(c)] = c
+        feats = fe.extract(torch.from_numpy(audio).to(dev))
+        toks = model.generate(feats, language="ja", task="transcribe", return_timestamps=True, max_length=128)
+        pad = model.generation_config.pad_token_id
+        passes += model.stats["row_passes"].tolist()
+        ntok += (toks != pad).sum(1).cpu().tolist()
+        print(f"batch {b0 // a.batch}: passes {model.stats['row_passes'].tolist()} ({time.time() - t0:.1f}s)",
+              flush=True)
+    passes = np.array(passes)
+    res = {"dtype": a.dtype, "n_clips": len(durs), "max_length": 128, "passes": passes.tolist(), "tokens": ntok,
+           "multipass_clips": np.nonzero(passes >= 2)[0].tolist(),
+           "histogram": {int(k): int((passes == k).sum()) for k in np.unique(passes)}}
+    os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
+    with open(a.out, "w") as f:
+        json.dump(res, f)
+    print(json.dumps({k: res[k] for k in ("n_clips", "histogram")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -408,8 +408,12 @@ def _stub_tokenizer(gen):
 
 
 def pipeline_audio(spec):
-    """"kind:seed:seconds" -> the seeded 30 s clips of ``kind`` concatenated and cut (long_audio)."""
+    """"kind:seed:seconds" -> the seeded 30 s clips of ``kind`` concatenated and cut (long_audio); kind "reazon":
+    clip ``seed`` of the config-4/5 stand-in at ``seconds`` (kwhisper.synthetic.reazon_audio, what
+    tools/bench_configs.py feeds config 5)."""
     kind, seed, sec = str(spec).split(":")
+    if kind == "reazon":
+        return S.reazon_audio(int(seed), float(sec))
     return long_audio(kind, int(seed), float(sec))
 
 
@@ -424,6 +428,10 @@ PIPE_CASES = {
     # BASELINE config 5 (run_short_form_eval.py:110-117,184-191 with chunk_length 15): kotoba-v2.0, beam 5
     "kotoba_v2": (KOTOBA_V2, ["tone:1:40", "dummy:5:12"], 15, 4,
                   dict(language="ja", task="transcribe", num_beams=5, max_length=40), (True,)),
+    # config 5 at its BASELINE batch: 22 of tools/bench_configs.py's 30 s clips -> 66 windows,
+    # window batches of 64 + 2 (bs = 64: 320 beam rows), beam 5, timestamps, max_length 128 as bench_configs runs it
+    "kotoba_v2_b64": (KOTOBA_V2, [f"reazon:{i}:30" for i in range(22)], 15, 64,
+                      dict(language="ja", task="transcribe", num_beams=5, max_length=128), (True,)),
 }
 
 
@@ -505,6 +513,8 @@ def main():
         kotoba_beam_fixtures()
     if a.only in (None, "pipeline"):
         pipeline_fixtures(("tiny", "tiny_longform") if a.skip_large else ("tiny", "tiny_longform", "kotoba_v2"))
+    if not a.skip_large and a.only in (None, "pipeline_b64"):
+        pipeline_fixtures(("kotoba_v2_b64",))
     if not a.skip_large and a.only in (None, "kotoba"):
         cases = [("tone", 1), ("dummy", 2)]
         modes = [{"name": "greedy", "kw": dict(base, return_timestamps=False), "scores": True}]
