@@ -429,20 +429,26 @@ def test_pipeline_longform_tiny_batched(gold, tiny32):
 C4_KW = dict(language="ja", task="transcribe", return_timestamps=True, max_length=128)  # :99-102, max_label_length
 
 
-def _c4_features(durations, idx):
-    """Log-mel (oracle, f64 STFT) of config-4 stand-in clips ``idx`` zero-padded to 30 s, as the feature
-    extractor pads them (feature_extraction_whisper.py:300-307)."""
+def _c4_features(g):
+    """Log-mel (oracle, f64 STFT) of the fixture's config-4 stand-in clips zero-padded to 30 s, as the feature
+    extractor pads them (feature_extraction_whisper.py:300-307).  Clip i of the stand-in is
+    reazon_audio(i, duration); the fixture names its clips by ``clip_ids`` (the first 32 when absent)."""
     from kwhisper.synthetic import reazon_audio
     from oracle.mel import log_mel, pad_or_trim
 
-    clips = [pad_or_trim(reazon_audio(int(i), float(durations[int(i)]))) for i in idx]
+    ids = g["clip_ids"] if "clip_ids" in g else np.arange(len(g["durations"]))
+    clips = [pad_or_trim(reazon_audio(int(i), float(d))) for i, d in zip(ids, g["durations"])]
     return torch.from_numpy(log_mel(np.stack(clips), LARGE_V3.num_mel_bins)).cuda()
 
 
-@pytest.fixture(scope="module")
-def c4_gold(gold):
-    g = gold("large_v3_ts_b32_fp32")
-    return g, _c4_features(g["durations"], range(len(g["durations"])))
+# the first 32 stand-in clips (every row one seek pass), and a batch with >= 8 rows that take a second pass
+C4_FIXTURES = ["large_v3_ts_b32_fp32", "large_v3_ts_mp_b32_fp32"]
+
+
+@pytest.fixture(scope="module", params=C4_FIXTURES)
+def c4_gold(gold, request):
+    g = gold(request.param)
+    return request.param, g, _c4_features(g)
 
 
 def _c4_pseudo_label(model, durations, feats_all, batch_size):
@@ -457,25 +463,31 @@ def _c4_pseudo_label(model, durations, feats_all, batch_size):
 def test_config4_fp32_pseudo_label_bitexact(c4_gold):
     """Config 4 at its own teacher in the fp32 parity mode: pseudo_label() (W = 1, batch 32) over large-v3 with
     timestamps returns transformers' fp32 tokens exactly, row for row (the split timestamp sampler at
-    V = 51866, B = 32, and the seek loop over zero-padded short clips)."""
-    g, feats = c4_gold
+    V = 51866, B = 32, and the seek loop over zero-padded short clips).  On the multi-pass fixture >= 8 rows take
+    a second seek pass (a re-encode of the shifted mel, generation_whisper.py:785-903, with the cumulative
+    max_length growth :1935-1940), and the engine's per-row pass counts equal transformers'."""
+    name, g, feats = c4_gold
     model = _model(LARGE_V3, torch.float32)
     ids, preds = _c4_pseudo_label(model, g["durations"], feats, 32)
     assert ids == list(range(32))
     np.testing.assert_array_equal(np.stack(preds), g["tokens"])
     assert model.stats["passes"] == int(g["passes"].max())
+    np.testing.assert_array_equal(model.stats["row_passes"], g["passes"])
+    if name == "large_v3_ts_mp_b32_fp32":
+        assert int((g["passes"] >= 2).sum()) >= 8
+        print(f"\nconfig4 multi-pass fixture: seek passes per row {g['passes'].tolist()}; fp32 engine bit-exact")
     del model
     _free()
 
 
-def _c4_worker(rank, world, port, out_dir, batch_size):
+def _c4_worker(rank, world, port, out_dir, batch_size, name):
     import torch.distributed as dist
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
-        g = np.load(os.path.join(os.path.dirname(__file__), "golden", "large_v3_ts_b32_fp32.npz"))
+        g = dict(np.load(os.path.join(os.path.dirname(__file__), "golden", f"{name}.npz")))
         model = _model(LARGE_V3, torch.bfloat16)
-        feats = _c4_features(g["durations"], range(len(g["durations"])))
+        feats = _c4_features(g)
         ids, preds = _c4_pseudo_label(model, g["durations"], feats, batch_size)
         np.savez(os.path.join(out_dir, f"c4_r{rank}.npz"), ids=np.array(ids), preds=np.stack(preds))
     finally:
@@ -490,7 +502,7 @@ def test_config4_bf16_pseudo_label_w1_w2(c4_gold, tmp_path):
     batch-invariant: each row's arithmetic does not depend on its batch)."""
     import torch.multiprocessing as mp
 
-    g, feats = c4_gold
+    name, g, feats = c4_gold
     model = _model(LARGE_V3, torch.bfloat16)
     ids1, preds1 = _c4_pseudo_label(model, g["durations"], feats, 32)
     assert ids1 == list(range(32))
@@ -498,15 +510,16 @@ def test_config4_bf16_pseudo_label_w1_w2(c4_gold, tmp_path):
     want = g["tokens"]
     assert toks.shape == want.shape
     n = _gated_equal(toks, want, g["margin"])
-    print(f"\nconfig4 bf16 pseudo_label (large-v3, B = 32, timestamps): {n} of {want.size} tokens compared "
+    print(f"\nconfig4 bf16 pseudo_label ({name}: large-v3, B = 32, timestamps): {n} of {want.size} tokens compared "
           f"(margin >= {MARGIN_FLOOR}), all equal; {int((toks == want).all(1).sum())}/32 rows identical; "
-          f"{(toks == want).mean():.4f} of positions equal; seek passes {model.stats['passes']}")
+          f"{(toks == want).mean():.4f} of positions equal; seek passes {model.stats['passes']} (per row "
+          f"{model.stats['row_passes'].tolist()}, reference {g['passes'].tolist()})")
     del model
     _free()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.spawn(_c4_worker, args=(2, port, str(tmp_path), 16), nprocs=2, join=True)
+    mp.spawn(_c4_worker, args=(2, port, str(tmp_path), 16, name), nprocs=2, join=True)
     for r in range(2):
         z = np.load(tmp_path / f"c4_r{r}.npz")
         assert z["ids"].tolist() == list(range(32))

@@ -118,9 +118,55 @@ def two_layer():
     g_il.replay()
 
 
+def masked_stream(bits):
+    """A HIP stream restricted to the CUs whose bits are set (hipExtStreamCreateWithCUMask through ctypes on the
+    HIP runtime torch has loaded), wrapped for torch."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(0).multi_processor_count
+    words = (ncu + 31) // 32
+    mask = (ctypes.c_uint32 * words)()
+    for c in range(ncu):
+        if bits(c):
+            mask[c // 32] |= 1 << (c % 32)
+    st = ctypes.c_void_p()
+    rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(st), ctypes.c_uint32(words), mask)
+    assert rc == 0, rc
+    return torch.cuda.ExternalStream(st.value)
+
+
+ncu = torch.cuda.get_device_properties(0).multi_processor_count
+masks = {"contiguous halves": (lambda c: c < ncu // 2, lambda c: c >= ncu // 2),
+         "even / odd CUs": (lambda c: c % 2 == 0, lambda c: c % 2 == 1)}
+masked = {}
+for name, (ma, mb) in masks.items():
+    ms_a, ms_b = masked_stream(ma), masked_stream(mb)
+
+    def run(ms_a=ms_a, ms_b=ms_b):
+        ms_a.wait_stream(cur)
+        ms_b.wait_stream(cur)
+        with torch.cuda.stream(ms_a):
+            g_a.replay()
+        with torch.cuda.stream(ms_b):
+            g_b.replay()
+        cur.wait_stream(ms_a)
+        cur.wait_stream(ms_b)
+
+    def run_one(ms_a=ms_a):
+        ms_a.wait_stream(cur)
+        with torch.cuda.stream(ms_a):
+            g_a.replay()
+        cur.wait_stream(ms_a)
+
+    masked[name] = (run, run_one)
+
 bench("one session", one, 1)
 bench("two sessions, free-running streams", two_free, 2)
 bench("two sessions, layer-interleaved graph", two_layer, 2)
+for name, (run, run_one) in masked.items():
+    bench(f"one session on half the CUs ({name})", run_one, 1)
+    bench(f"two sessions, CU-masked ({name})", run, 2)
 bench("one session (again)", one, 1)
 res["gain_free"] = round(res["one session"] / res["two sessions, free-running streams"], 4)
 res["gain_layer"] = round(res["one session"] / res["two sessions, layer-interleaved graph"], 4)

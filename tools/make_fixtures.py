@@ -350,6 +350,48 @@ def large_config4_fixtures():
     print(f"large_v3_ts_b32 fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
 
 
+def large_config4_multipass_fixtures(ids_json):
+    """tests/golden/large_v3_ts_mp_b32_fp32.npz: config 4 at its own teacher on a 32-clip batch in which at least
+    8 clips take a SECOND seek pass (the first 32 stand-in clips all finish in one).  The clip
+    ids come from ``ids_json`` (tools/find_multipass.py's output over the fp32 engine, bit-exact with transformers):
+    the first 16 multi-pass clips plus the first 16 single-pass ones, in id order.  transformers' fp32 large-v3 then
+    decodes that batch with the reference's settings (run_pseudo_labelling.py:99-102,338; max_length 128, the
+    cumulative growth generation_whisper.py:1935-1940): tokens, per-token margins through the seek passes, passes
+    per row, segments."""
+    t0 = time.time()
+    with open(ids_json) as f:
+        found = json.load(f)
+    passes_found = np.asarray(found["passes"])
+    multi = [int(i) for i in np.nonzero(passes_found >= 2)[0][:16]]
+    single = [int(i) for i in np.nonzero(passes_found == 1)[0][:32 - len(multi)]]
+    ids = sorted(multi + single)
+    assert len(ids) == 32 and len(multi) >= 8, (len(ids), len(multi))
+    durs_all = S.reazon_durations()
+    durs = durs_all[ids]
+    audio = [S.reazon_audio(i, float(durs_all[i])) for i in ids]
+    fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins)
+    feats = torch.from_numpy(fe(audio, sampling_rate=16000, return_tensors="np")["input_features"])
+    m = hf_model(LARGE_V3)
+    m.generation_config, gc = hf_gen_config(LARGE_V3)
+    kw = dict(language="ja", task="transcribe", return_timestamps=True, max_length=128)
+    res = run_generate(m, feats, return_dict_in_generate=True, output_scores=True, **kw)
+    print(f"  large_v3_ts_mp_b32: generate ({time.time() - t0:.1f}s)")
+    toks = res["sequences"].numpy().astype(np.int64)
+    P = 3
+    margin = np.full(toks.shape, np.inf, np.float32)
+    passes = np.zeros(len(audio), np.int64)
+    for b, segs in enumerate(res["segments"]):
+        mg, tk, passes[b] = _aligned_margins(segs, P)
+        assert np.array_equal(tk, toks[b, : len(tk)]) and (toks[b, len(tk):] == gc.pad_token_id).all()
+        margin[b, : len(mg)] = mg
+    segs = [[(float(x["start"]), float(x["end"]), len(x["tokens"])) for x in row] for row in res["segments"]]
+    out = {"clip_ids": np.asarray(ids, np.int64), "durations": durs.astype(np.float64), "tokens": toks,
+           "margin": margin, "passes": passes, "engine_passes": passes_found[ids].astype(np.int64),
+           "segments": np.array(json.dumps(segs)), "max_length": 128}
+    np.savez_compressed(os.path.join(GOLD, "large_v3_ts_mp_b32_fp32.npz"), **out)
+    print(f"large_v3_ts_mp_b32 fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
+
+
 KOTOBA_BEAM_CASES = [("tone", 0), ("dummy", 0), ("tone", 2), ("dummy", 3)]
 KOTOBA_BEAM_MODES = [
     ("beam5_ts", dict(language="ja", task="transcribe", return_timestamps=True, num_beams=5, max_length=48)),
@@ -473,6 +515,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
     ap.add_argument("--only", default=None)
+    ap.add_argument("--multipass-ids", default="profiles/r04_multipass_clips.json",
+                    help="--only large_c4_mp: tools/find_multipass.py output naming the multi-pass clips")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     torch.manual_seed(0)
@@ -509,6 +553,8 @@ def main():
         large_bf16_ref_fixtures()
     if not a.skip_large and a.only in (None, "large_c4"):
         large_config4_fixtures()
+    if not a.skip_large and a.only == "large_c4_mp":
+        large_config4_multipass_fixtures(a.multipass_ids)
     if not a.skip_large and a.only in (None, "kotoba_beam"):
         kotoba_beam_fixtures()
     if a.only in (None, "pipeline"):
