@@ -1,7 +1,8 @@
 """Rank script for tests/test_gpu_dist.py: kwhisper.pseudo_label under torch.distributed.run with the RCCL
 ("nccl") backend -- init_process_group(device_id=...), the per-round width all_reduce(MAX) and id all_gathers
-(gather="round", run_pseudo_labelling.py:339-341) and the deferred exchange (gather="end") -- over the tiny bf16
-engine, against the same loop without a process group.  Prints one JSON line on rank 0."""
+(gather="round", run_pseudo_labelling.py:339-341) and the deferred exchange (gather="end") -- and the ASR
+pipeline's data-parallel window batches, over the tiny bf16 engine, against the same calls without a process
+group.  Prints one JSON line on rank 0."""
 import json
 import os
 import sys
@@ -46,6 +47,14 @@ def main():
     for mode in ("round", "end"):
         ids, preds = pseudo_label(model, features, n, batch_size=bs, gen_kwargs=kw, pad_token_id=pad, gather=mode)
         out[mode] = bool(ids == ref_ids and len(preds) == len(ref) and all(np.array_equal(a, b) for a, b in zip(preds, ref)))
+    # the ASR pipeline's window batches under the process group (config 5 at W GPUs): one gather at the end
+    from kwhisper.pipeline import ASRPipeline
+
+    clips = [{"array": reazon_audio(50 + i, 40.0 - 9 * i), "sampling_rate": 16000} for i in range(3)]
+    kwp = dict(chunk_length_s=15, batch_size=2, generate_kwargs=dict(language="ja", task="transcribe", max_length=32))
+    dp = ASRPipeline(model, **kwp)(clips, return_timestamps=True)
+    single = ASRPipeline(model, data_parallel=False, **kwp)(clips, return_timestamps=True)
+    out["pipeline"] = json.dumps(dp, default=str) == json.dumps(single, default=str)
     dist.barrier()
     dist.destroy_process_group()
     if int(os.environ.get("RANK", "0")) == 0:

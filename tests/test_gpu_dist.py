@@ -46,8 +46,8 @@ def test_bench_rank_code_over_rccl():
 
 
 def test_pseudo_label_over_rccl():
-    """pseudo_label's per-round collectives and the deferred exchange over RCCL return the single-process
-    predictions."""
+    """pseudo_label's per-round collectives and the deferred exchange, and the ASR pipeline's data-parallel
+    gather, over RCCL return the single-process results."""
     r = _torchrun(os.path.join(ROOT, "tests", "_dist_pl.py"))
     print("\npseudo_label over RCCL:", r)
-    assert r["backend"] == "nccl" and r["world"] == 1 and r["round"] and r["end"]
+    assert r["backend"] == "nccl" and r["world"] == 1 and r["round"] and r["end"] and r["pipeline"]

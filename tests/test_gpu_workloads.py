@@ -122,7 +122,23 @@ def test_config3_bf16_generate_b32(gold, large_b32_gold):
           f"{ref_err.max():.4f} mean {ref_err.mean():.5f}")
     assert err[rows].max() <= ref_err.max() and err[rows].mean() <= ref_err.mean()
     assert err.max() < 0.2 and err.mean() < 0.03
-    del lg, sess
+    # teacher-forced greedy choice at EVERY step the fp32 reference decides by a margin >= MARGIN_FLOOR (the fed
+    # sequence keeps the engine on the reference trajectory past any earlier low-margin step): the processed
+    # argmax (SuppressTokens, SuppressTokensAtBegin at the first step; logits_process.py:1816-1906) equals the
+    # fp32 reference's token
+    gen = generation_constants(LARGE_V3)
+    n_pos = g["greedy_margin"].shape[1]
+    proc = lg[:, :n_pos].clone()
+    proc[:, :, torch.tensor(gen.suppress_tokens, device=proc.device)] = -float("inf")
+    proc[:, 0, torch.tensor(gen.begin_suppress_tokens, device=proc.device)] = -float("inf")
+    choice = proc.argmax(-1).cpu().numpy()
+    want_tok = g["greedy_sequences"][:, 4: 4 + n_pos]
+    safe = g["greedy_margin"] >= MARGIN_FLOOR
+    bad = np.argwhere(safe & (choice != want_tok))
+    print(f"config3 bf16 teacher-forced greedy choice: {int(safe.sum())} of {safe.size} steps with fp32 margin >= "
+          f"{MARGIN_FLOOR} compared, {len(bad)} differ; all steps agree at {(choice == want_tok).mean():.4f}")
+    assert len(bad) == 0, f"(row, step) pairs whose safe-margin greedy choice differs: {bad[:8].tolist()}"
+    del lg, proc, sess
     _free()
     # the graph-replayed generate() (what bench.py times)
     toks = model.generate(feats, language="ja", task="transcribe", max_length=128).cpu().numpy()
@@ -147,8 +163,8 @@ def test_config3_bf16_generate_b32(gold, large_b32_gold):
     # equal positions: no worse than the reference's own bf16 model.  The mean first-divergence step of 32 greedy
     # trajectories moves by a few steps with any change of summation order at equal teacher-forced error (71.4
     # and 68.3 for two cross-attention kernels whose logit errors are 0.0914 / 0.0229 and 0.0899 / 0.0230, HF
-    # bf16 71.0): held within 10 % of the reference bf16 model's
-    assert ours_eq >= ref_eq and ours_fd.mean() >= 0.9 * ref_fd.mean()
+    # bf16 71.0): held within 5 % of the reference bf16 model's (the per-step check above is the strict one)
+    assert ours_eq >= ref_eq and ours_fd.mean() >= 0.95 * ref_fd.mean()
     # batch invariance: two of the clips alone give the rows they get inside the batch of 32
     sub = [0, 17]
     toks2 = model.generate(feats[sub], language="ja", task="transcribe", max_length=128).cpu().numpy()

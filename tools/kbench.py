@@ -63,7 +63,10 @@ def main():
     ap.add_argument("--eager", action="store_true", help="no graph, no timing (for rocprofv3 --pmc passes)")
     ap.add_argument("--warm", action="store_true", help="one weight buffer per linear (L2/MALL-warm replays)")
     ap.add_argument("--self-t", default="132", help="comma list of self-attention lengths (cur_len) to time")
+    ap.add_argument("--backend", default="torch", choices=("torch", "ctypes"),
+                    help="ctypes: call the C ABI directly (with KWHISPER_LIB=<lab build> for geometry overrides)")
     a = ap.parse_args()
+    ops.set_backend(a.backend)
     global EAGER
     EAGER = a.eager
     only = set(filter(None, a.only.split(",")))
