@@ -633,7 +633,7 @@ __device__ __forceinline__ void attend_rows(const float qv[8], int k0, int k1, K
       const int k = kb + 32 * j;
       const float pk = k < k1 ? sc[k - k0] : 0.f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pk, vv[j][i], acc[i]);
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pk, k < k1 ? vv[j][i] : 0.f, acc[i]);  // (stale masked rows)
     }
   }
 #pragma unroll
@@ -721,12 +721,13 @@ __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, 
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (act(j)) {
-      const float pj = (k0 + slot + 32 * j < k1) ? expf(sc[j] - m) : 0.f;
+      const bool valid = k0 + slot + 32 * j < k1;
+      const float pj = valid ? expf(sc[j] - m) : 0.f;
       lsum += pj;
       float vv[8];
       unpack8<T>(vr[j], vv);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, vv[i], acc[i]);
+      for (int i = 0; i < 8; ++i) acc[i] = fmaf(pj, valid ? vv[i] : 0.f, acc[i]);  // (stale masked rows: see wave_values_bf16)
     }
   }
   // lanes of one wave with equal sub hold the same dims: reduce over lane bits 3..5

@@ -80,9 +80,13 @@ __device__ __forceinline__ void wave_values_bf16(const float sc[8], float mx, co
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (j < nj) {
-      const float pj = (k0 + slot + KS * j < k1) ? __builtin_amdgcn_exp2f(sc[j] - mx) : 0.f;
+      const bool valid = k0 + slot + KS * j < k1;
+      const float pj = valid ? __builtin_amdgcn_exp2f(sc[j] - mx) : 0.f;
       lsum += pj;
-      const uint32_t w[4] = {vr[j][0], vr[j][1], vr[j][2], vr[j][3]};
+      // a masked slot holds a clamped row that may be STALE (a cache row this step has not written yet, e.g. the
+      // new position's row before its append): p = 0 times a stale NaN / Inf is NaN, so its values are zeroed
+      const uint32_t w[4] = {valid ? vr[j][0] : 0u, valid ? vr[j][1] : 0u, valid ? vr[j][2] : 0u,
+                             valid ? vr[j][3] : 0u};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         acc[2 * i] = fmaf(pj, __uint_as_float(w[i] << 16), acc[2 * i]);
