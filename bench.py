@@ -119,6 +119,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--kernel-iters", type=int, default=20)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="extra measurement (not the headline value): this many bs-32 batches decoding at once, one "
+                         "host thread and stream each over engine lanes sharing the weights; 1 = skip")
     ap.add_argument("--stub", action="store_true",
                     help="no GPU work: each rank times a trivial host step (tests the launcher, barriers, "
                          "max-over-ranks timing and the ids gather on the CPU; with KW_BENCH_BACKEND=gloo)")
@@ -278,6 +281,50 @@ def main(argv=None):
     if gathered is not None:
         assert len(gathered) == world and all(g.shape == gathered[0].shape for g in gathered)
 
+    def inflight_rate(n_lanes, n_batches):
+        """``n_lanes`` batches of B clips in flight at once (one thread, stream, model handle and decode session
+        each; the weights shared through WhisperEngine.lane()): one batch's latency-bound decode chain runs beside
+        another's HBM-bound cross-attention stream (tools/lab/dual_decode.py).  Every lane is warmed up (graphs
+        captured) before any thread starts, so no capture overlaps another thread's launches."""
+        import threading
+
+        lanes = [KWhisperForConditionalGeneration(model.engine.lane()) for _ in range(n_lanes)]
+        streams = [torch.cuda.Stream(device=dev) for _ in lanes]
+        ref = out_ids[-1].cpu()
+        for m, st in zip(lanes, streams):
+            with torch.cuda.stream(st):
+                got = m.generate(fe.extract(audio), **gen_kw)
+            st.synchronize()
+            assert torch.equal(got.cpu(), ref), "a lane's tokens differ from the sequential run's"
+        torch.cuda.synchronize()
+        errs = []
+
+        def work(m, st, k):
+            try:
+                with torch.cuda.stream(st):
+                    for _ in range(k):
+                        m.generate(fe.extract(audio), **gen_kw)
+                st.synchronize()
+            except BaseException as e:  # surfaced below
+                errs.append(e)
+
+        per = [n_batches // n_lanes + (1 if i < n_batches % n_lanes else 0) for i in range(n_lanes)]
+        threads = [threading.Thread(target=work, args=(m, st, k)) for m, st, k in zip(lanes, streams, per)]
+        t0 = time.perf_counter()
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+        torch.cuda.synchronize()
+        dt_ = time.perf_counter() - t0
+        if errs:
+            raise errs[0]
+        return {"lanes": n_lanes, "batches": n_batches, "value": n_batches * B * 30.0 / dt_,
+                "ms_per_batch": dt_ / n_batches * 1e3,
+                "note": "NOT the headline value: batches of 32 decoded concurrently, each generate() call at bs 32"}
+
+    inflight = inflight_rate(a.inflight, max(2 * a.inflight, a.steps)) if a.inflight > 1 and world == 1 else None
+
     # ---- per-kernel measurements (HIP events on the launching stream, after the timed region) ----
     eng = model.engine
     sess = model._sessions.get((B, 1)) or model._sessions[(B, 1, 1)]
@@ -384,6 +431,7 @@ def main(argv=None):
         "encoder_mfma": {"ms": enc_t * 1e3, "tflops": ENC_FLOP_PER_CLIP * B / enc_t / 1e12,
                          "frac": ENC_FLOP_PER_CLIP * B / enc_t / 1e12 / BF16_PEAK_TFLOPS},
         "decode_step_ms": step_t * 1e3 if step_t else None,
+        "inflight": inflight,
         "decode_kernel_us": kern_us,
         "decode_kernel_us_note": ("eager launches in step order with HIP events around each: includes the host "
                                   "dispatch gap a graph replay does not have; device times per kernel are the "

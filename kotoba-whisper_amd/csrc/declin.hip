@@ -840,6 +840,9 @@ Geo choose(int64_t N, int64_t K) {
   // 1280x1280 5.8 -> 5.1 us, fc1 9.0 -> 8.6 us (profiles/r01h_declin_geo_sweep.txt); the LM head and
   // the split fc2 (6 x 27 k-tiles over 3 waves, r01g_splitk_sweep.txt) keep 10
   g.ktm = (g.ks == 1 && per_wg0 <= 40 && (N < 8192 || per_wg0 <= 5)) ? 5 : 10;  // (K <= 160: the u projection)
+  // r04: the split fc2 (6 x 27 k-tiles) on 6 waves of 5 k-tiles instead of 3 of 10 -- more loads in flight per
+  // workgroup: 9.79-9.89 vs 10.27-10.29 us (profiles/r04c_splitk_sweep.txt; ks 8 / 4 and the o-proj split worse)
+  if (g.ks > 1 && per_wg0 <= 5 * MAXW && N < 8192) g.ktm = 5;
 #ifdef KW_LAB_OVERRIDES
   // lab builds only (make EXTRA=-DKW_LAB_OVERRIDES OUT=...; tools/lab/*_sweep.sh): KW_DECLIN_GEO="N,K,ncb,ktm,ks"
   // overrides one matrix shape's geometry; read once, thread-safe (function-local static)

@@ -9,7 +9,9 @@ A ``DecodeSession`` owns the static caches and step buffers of one batch:
 The prefill (prompt of P tokens) runs eagerly; the single-token step (embedding + 32 x 8 kernels +
 LM head with the final LayerNorm fused + sampler) is captured once into a hipGraph (torch.cuda.CUDAGraph) and replayed: the step
 reads its position from device memory, so one graph serves every step.  The host only polls the
-device unfinished-row count a few steps behind the GPU (no per-step sync).
+device unfinished-row count a few steps behind the GPU (no per-step sync).  Graphs are captured with
+capture_error_mode="thread_local", so another host thread (another batch in flight on its own stream,
+WhisperEngine.lane()) may keep launching while one session captures.
 """
 from __future__ import annotations
 
@@ -389,7 +391,7 @@ class DecodeSession:
             pg = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.graph(pg, stream=side):
+            with torch.cuda.graph(pg, stream=side, capture_error_mode="thread_local"):
                 prefill()
             torch.cuda.current_stream(dev).wait_stream(side)
             cfg["prefill_graph"] = pg
@@ -415,7 +417,7 @@ class DecodeSession:
             g = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(device=dev)
             side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.graph(g, stream=side):
+            with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                 for _ in range(n):
                     one_step()
             torch.cuda.current_stream(dev).wait_stream(side)
@@ -547,7 +549,7 @@ class DecodeSession:
                 g = torch.cuda.CUDAGraph()
                 side = torch.cuda.Stream(device=dev)
                 side.wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.graph(g, stream=side):
+                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
                     fn()
                 torch.cuda.current_stream(dev).wait_stream(side)
                 cfg[name] = g

@@ -328,6 +328,16 @@ class WhisperEngine:
                      hs_seq=T, hs_heads=self.H, hs_head_dim=_HD)()
         return out
 
+    def lane(self) -> "WhisperEngine":
+        """Another handle on this engine's weights with its own activation buffers and side streams, so a second
+        host thread can run batches at the same time as this one (each thread on its own current stream, each
+        with its own KWhisperForConditionalGeneration and decode sessions).  Nothing is copied on the device."""
+        import copy
+
+        other = copy.copy(self)
+        other._enc, other._enc_split, other._enc_streams = {}, {}, []
+        return other
+
     def new_session(self, B: int, enc: torch.Tensor | None = None, beams: int = 1) -> "DecodeSession":
         from .decode import DecodeSession
 

@@ -100,6 +100,13 @@ class KWhisperForConditionalGeneration:
     def get_encoder(self):
         return _Encoder(self.engine)
 
+    def lane(self) -> "KWhisperForConditionalGeneration":
+        """An independent handle on the same weights (WhisperEngine.lane(): own activation buffers, streams and decode
+        sessions) for running another batch at the same time from another host thread."""
+        other = type(self)(self.engine.lane())
+        other.generation_config = copy.deepcopy(self.generation_config)
+        return other
+
     @classmethod
     def from_state_dict(cls, shape, state_dict, *, dtype=torch.bfloat16, device="cuda", generation_config=None):
         shape = PRESETS[shape] if isinstance(shape, str) else shape

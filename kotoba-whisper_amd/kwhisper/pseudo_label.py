@@ -326,20 +326,51 @@ def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, com
     done = _done_rounds(checkpoint_dir, n_steps, dev,
                         {"n_items": int(n_items), "batch_size": int(batch_size), "world_size": int(world),
                          "config_sha256": digest, "gather": "end"}, rank_files=world)
-    local: List[List[np.ndarray]] = []  # [step][column] -> (batch_size, width) int64
-    for si, idx in enumerate(steps):
+    decoders = decode if isinstance(decode, (list, tuple)) else [decode]
+    local: List[Optional[List[np.ndarray]]] = [None] * n_steps  # [step][column] -> (batch_size, width) int64
+
+    def run_step(si, dec):
+        idx = steps[si]
         path = _rank_round_path(checkpoint_dir, si, rank) if checkpoint_dir else None
         if done[si]:
             _, mats = _load_round(checkpoint_dir, si, path)
         else:
-            mats = [o.cpu().numpy().astype(np.int64) for o in decode(features(idx))]
+            mats = [o.cpu().numpy().astype(np.int64) for o in dec(features(idx))]
             if checkpoint_dir:
                 _save_round(checkpoint_dir, si, list(idx), mats, path)
-        if local and len(mats) != len(local[0]):
-            raise ValueError(f"step {si} produced {len(mats)} output columns, earlier steps {len(local[0])}")
-        local.append(mats)
+        local[si] = mats
         if on_step is not None:
             on_step(si, n_steps)
+
+    if len(decoders) == 1:
+        for si in range(n_steps):
+            run_step(si, decoders[0])
+    else:  # lanes: step si on lane si % n (one host thread each); lane i's first step runs alone first, so every
+        # lane's graphs are captured before the threads overlap
+        import threading
+
+        n = len(decoders)
+        for si in range(min(n, n_steps)):
+            run_step(si, decoders[si])
+        errs: List[BaseException] = []
+
+        def lane_work(i):
+            try:
+                for si in range(i + n, n_steps, n):
+                    run_step(si, decoders[i])
+            except BaseException as e:  # re-raised on the calling thread
+                errs.append(e)
+
+        threads = [threading.Thread(target=lane_work, args=(i,)) for i in range(n)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+        if errs:
+            raise errs[0]
+    for si, mats in enumerate(local):
+        if len(mats) != len(local[0]):
+            raise ValueError(f"step {si} produced {len(mats)} output columns, earlier steps {len(local[0])}")
     n_cols = len(local[0]) if local else 0
     if dist is not None:  # every rank runs the same number of steps (even_batches): agree on the column count
         t = torch.tensor([n_cols], dtype=torch.int64, device=dev)
@@ -400,6 +431,18 @@ def gather_matrices(mats: Sequence[np.ndarray], n_slots: int, pad: int, device=N
 _GATHER = {"round": _label_loop, "end": _label_loop_deferred}
 
 
+def _lane_models(model, lanes: int, gather: str):
+    if lanes < 1:
+        raise ValueError("lanes must be >= 1")
+    if lanes == 1:
+        return [model]
+    if gather != "end":
+        raise ValueError("lanes > 1 needs gather='end' (the per-round gather keeps one batch in flight)")
+    if not hasattr(model, "lane"):
+        raise ValueError("lanes > 1 needs a model with lane() (an independent handle on the same weights)")
+    return [model] + [model.lane() for _ in range(lanes - 1)]
+
+
 def _loop(gather):
     try:
         return _GATHER[gather]
@@ -410,7 +453,7 @@ def _loop(gather):
 def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *, batch_size: int,
                  pad_token_id: int, gen_kwargs: Optional[dict] = None, comm_device=None,
                  on_step: Optional[Callable[[int, int], None]] = None, legacy_prompt_in_output: bool = False,
-                 checkpoint_dir: Optional[str] = None, gather: str = "round"):
+                 checkpoint_dir: Optional[str] = None, gather: str = "round", lanes: int = 1):
     """Transcribe items 0..n_items-1 data-parallel; returns (item_indices, predictions) in dataset order
     on every rank (``run_pseudo_labelling.py:333-344``).
 
@@ -424,9 +467,14 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
     ``legacy_prompt_in_output`` prepends ``legacy_prompt(...)`` to every row (needs ``language``).
     ``checkpoint_dir``: checkpoint every gathered round there and skip rounds already written (resume).
     ``gather``: "round" pads and gathers after every batch as the reference does; "end" defers every collective
-    to one exchange after the rank's last batch (``_label_loop_deferred``: the same predictions, no lock step)."""
+    to one exchange after the rank's last batch (``_label_loop_deferred``: the same predictions, no lock step).
+    ``lanes`` > 1 (with gather="end"): that many of the rank's batches decode at once, each batch still
+    ``batch_size`` items, on ``model.lane()`` handles (shared weights, one host thread and stream each): one
+    batch's latency-bound decode chain overlaps another's HBM-bound cross-attention (tools/lab/dual_decode.py).
+    The predictions are the same."""
     gen_kwargs = dict(gen_kwargs or {})
     loop = _loop(gather)
+    models = _lane_models(model, lanes, gather)
     prompt = None
     if legacy_prompt_in_output:
         if not gen_kwargs.get("language"):
@@ -434,14 +482,18 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
         prompt = legacy_prompt(model.generation_config, gen_kwargs["language"], gen_kwargs.get("task") or "transcribe",
                                bool(gen_kwargs.get("return_timestamps")))
 
-    def decode(feats):
-        ids = model.generate(feats, **gen_kwargs)
-        return [_with_prompt(ids, prompt) if prompt else ids]
+    def decoder(m):
+        def decode(feats):
+            ids = m.generate(feats, **gen_kwargs)
+            return [_with_prompt(ids, prompt) if prompt else ids]
+
+        return decode
 
     digest = run_digest(model, gen_kwargs=gen_kwargs, pad_token_id=int(pad_token_id),
                         legacy_prompt_in_output=bool(legacy_prompt_in_output)) if checkpoint_dir else None
-    eval_ids, cols = loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                          checkpoint_dir, digest)
+    decs = [decoder(m) for m in models]
+    eval_ids, cols = loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step,
+                          decs if len(decs) > 1 else decs[0], checkpoint_dir, digest)
     return eval_ids, (cols[0] if cols else [])
 
 

@@ -397,3 +397,31 @@ def test_resume_accepts_legacy_plan_without_digest(tmp_path):
         got = pseudo_label(m, _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=str(ck))
     _same(got, ref)
     assert m.batches == []
+
+
+class _LaneStub(_CountingModel):
+    """A stub with lane(): each lane records its own batches (the engine lanes share weights, not sessions)."""
+
+    def __init__(self, lanes=None):
+        super().__init__()
+        self.lanes = lanes if lanes is not None else [self]
+
+    def lane(self):
+        other = _LaneStub(self.lanes)
+        self.lanes.append(other)
+        return other
+
+
+@pytest.mark.parametrize("n,bs,lanes", [(23, 4, 2), (23, 4, 3), (5, 4, 2), (0, 4, 2)])
+def test_lanes_return_the_single_lane_predictions(n, bs, lanes):
+    """lanes > 1 (gather="end"): batches decode on several model handles from several host threads; the predictions
+    (and their order) equal the single-lane run's, and every batch is decoded exactly once."""
+    ref = pseudo_label(_StubModel(), _features, n, batch_size=bs, pad_token_id=PAD, gather="end")
+    m = _LaneStub()
+    got = pseudo_label(m, _features, n, batch_size=bs, pad_token_id=PAD, gather="end", lanes=lanes)
+    _same(got, ref)
+    decoded = sorted(i for lane in m.lanes for b in lane.batches for i in b)
+    want = sorted(i for b in shard_batches(n, bs, 1, 0) for i in b)
+    assert decoded == want and len(m.lanes) == lanes
+    with pytest.raises(ValueError, match="gather"):
+        pseudo_label(_LaneStub(), _features, 3, batch_size=4, pad_token_id=PAD, lanes=2)

@@ -91,7 +91,7 @@ def config4(a, world, rank, dev):
     t0 = time.perf_counter()
     ids, preds = pseudo_label(model, features, n, batch_size=a.batch, gen_kwargs=gen_kw, gather=a.gather,
                               pad_token_id=model.generation_config.eos_token_id,  # tokenizer pad = <|endoftext|>
-                              on_step=on_step)
+                              on_step=on_step, lanes=a.lanes)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -104,9 +104,10 @@ def config4(a, world, rank, dev):
             "dtype": "bf16", "data": "synthetic (ReazonSpeech-tiny duration statistics, noise audio, random weights)",
             "config": {"workload": "config 4: run_pseudo_labelling.py loop, whisper-large-v3, timestamps, greedy",
                        "per_gpu_batch": a.batch, "max_length": a.max_length, "parallelism": f"dp{world}",
-                       "gather": a.gather, "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))},
+                       "gather": a.gather, "lanes": a.lanes,
+                       "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))},
             "batch_seconds": [round(float(x), 5) for x in batch_s], "batch_seek_passes": passes,
-            "dp_projection": dp_projection(batch_s) if world == 1 else None}
+            "dp_projection": dp_projection(batch_s) if world == 1 and a.lanes == 1 else None}
 
 
 def dp_projection(batch_s, worlds=(2, 4, 8)):
@@ -175,6 +176,8 @@ def main():
     ap.add_argument("--max-length", type=int, default=128)
     ap.add_argument("--gather", choices=("round", "end"), default="end",
                     help="config 4: the reference's per-batch gather (round) or one exchange at the end")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="config 4: batches of --batch in flight per GPU (pseudo_label lanes; needs --gather end)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -392,6 +392,43 @@ def large_config4_multipass_fixtures(ids_json):
     print(f"large_v3_ts_mp_b32 fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
 
 
+LARGE_LONG_CLIPS = [("tone", 0, 45.0), ("dummy", 3, 70.0)]
+
+
+def large_longform_fixtures():
+    """tests/golden/large_v3_longform_fp32.npz: the seek loop's SECOND and later passes at large-v3 (VERDICT r3 item
+    1).  No config-4 stand-in clip takes a second pass in transformers' fp32 large-v3 at max_length 128 (every one of
+    the 1,768 clips is single-pass: profiles/r04d_multipass_scan.json), so the multi-pass path -- re-encoding the mel
+    shifted to the last timestamp, the cumulative max_length growth (generation_whisper.py:785-903,1935-1940), the
+    shrinking batch -- is pinned on > 30 s clips, where every row takes several passes: two clips batched with the
+    frame attention mask (the run_pseudo_labelling timestamp settings: ja / transcribe, max_length 128), tokens,
+    per-token margins through the passes, passes per row, segments."""
+    t0 = time.time()
+    m = hf_model(LARGE_V3)
+    fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins)
+    audio = [long_audio(k, s, sec) for k, s, sec in LARGE_LONG_CLIPS]
+    inp = fe(audio, sampling_rate=16000, return_tensors="pt", truncation=False, padding="longest",
+             return_attention_mask=True)
+    m.generation_config, gc = hf_gen_config(LARGE_V3)
+    res = run_generate(m, inp["input_features"], attention_mask=inp["attention_mask"], return_timestamps=True,
+                       language="ja", task="transcribe", max_length=128, return_dict_in_generate=True,
+                       output_scores=True)
+    print(f"  large_v3_longform: generate ({time.time() - t0:.1f}s)")
+    toks = res["sequences"].numpy().astype(np.int64)
+    P = 3
+    margin = np.full(toks.shape, np.inf, np.float32)
+    passes = np.zeros(len(audio), np.int64)
+    for b, segs in enumerate(res["segments"]):
+        mg, tk, passes[b] = _aligned_margins(segs, P)
+        assert np.array_equal(tk, toks[b, : len(tk)]) and (toks[b, len(tk):] == gc.pad_token_id).all()
+        margin[b, : len(mg)] = mg
+    segs = [[(float(x["start"]), float(x["end"]), len(x["tokens"])) for x in row] for row in res["segments"]]
+    out = {"clips": np.array([f"{k}:{s}:{sec}" for k, s, sec in LARGE_LONG_CLIPS]), "tokens": toks, "margin": margin,
+           "passes": passes, "segments": np.array(json.dumps(segs)), "max_length": 128}
+    np.savez_compressed(os.path.join(GOLD, "large_v3_longform_fp32.npz"), **out)
+    print(f"large_v3_longform fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
+
+
 KOTOBA_BEAM_CASES = [("tone", 0), ("dummy", 0), ("tone", 2), ("dummy", 3)]
 KOTOBA_BEAM_MODES = [
     ("beam5_ts", dict(language="ja", task="transcribe", return_timestamps=True, num_beams=5, max_length=48)),
@@ -474,6 +511,10 @@ PIPE_CASES = {
     # window batches of 64 + 2 (bs = 64: 320 beam rows), beam 5, timestamps, max_length 128 as bench_configs runs it
     "kotoba_v2_b64": (KOTOBA_V2, [f"reazon:{i}:30" for i in range(22)], 15, 64,
                       dict(language="ja", task="transcribe", num_beams=5, max_length=128), (True,)),
+    # the same pipeline with the model in bfloat16, as run_short_form_eval.py runs it on a GPU (torch_dtype bf16,
+    # :110-117): the REFERENCE's own bf16 beam choices, the noise floor the bf16 engine is held to
+    "kotoba_v2_b64_bf16": (KOTOBA_V2, [f"reazon:{i}:30" for i in range(22)], 15, 64,
+                           dict(language="ja", task="transcribe", num_beams=5, max_length=128), (True,), torch.bfloat16),
 }
 
 
@@ -486,8 +527,10 @@ def pipeline_fixtures(tags=("tiny", "tiny_longform", "kotoba_v2")):
 
     for tag in tags:
         t0 = time.time()
-        shape, clips, chunk_s, bs, gk, ts_modes = PIPE_CASES[tag]
+        shape, clips, chunk_s, bs, gk, ts_modes = PIPE_CASES[tag][:6]
         m = hf_model(shape)
+        if len(PIPE_CASES[tag]) > 6:
+            m = m.to(PIPE_CASES[tag][6])  # the pipeline casts the features to the model's dtype (chunk_iter :73-74)
         m.generation_config, gen = hf_gen_config(shape)
         rec = _RecordingGenerate(m)
         m.generate = rec
@@ -507,8 +550,11 @@ def pipeline_fixtures(tags=("tiny", "tiny_longform", "kotoba_v2")):
             out[f"{key}_n_calls"] = len(rec.calls)
             for i, c in enumerate(rec.calls):
                 out[f"{key}_call{i}"] = c
+            if len(PIPE_CASES[tag]) > 6:
+                out["dtype"] = str(PIPE_CASES[tag][6])
             print(f"  pipeline_{tag}:{key} {len(rec.calls)} window batches ({time.time() - t0:.1f}s)")
-        np.savez_compressed(os.path.join(GOLD, f"pipeline_{tag}_fp32.npz"), **out)
+        suffix = "" if len(PIPE_CASES[tag]) > 6 else "_fp32"  # (the bf16 case's tag says its dtype)
+        np.savez_compressed(os.path.join(GOLD, f"pipeline_{tag}{suffix}.npz"), **out)
 
 
 def main():
@@ -553,6 +599,8 @@ def main():
         large_bf16_ref_fixtures()
     if not a.skip_large and a.only in (None, "large_c4"):
         large_config4_fixtures()
+    if not a.skip_large and a.only == "large_longform":
+        large_longform_fixtures()
     if not a.skip_large and a.only == "large_c4_mp":
         large_config4_multipass_fixtures(a.multipass_ids)
     if not a.skip_large and a.only in (None, "kotoba_beam"):
@@ -561,6 +609,8 @@ def main():
         pipeline_fixtures(("tiny", "tiny_longform") if a.skip_large else ("tiny", "tiny_longform", "kotoba_v2"))
     if not a.skip_large and a.only in (None, "pipeline_b64"):
         pipeline_fixtures(("kotoba_v2_b64",))
+    if not a.skip_large and a.only in (None, "pipeline_b64_bf16"):
+        pipeline_fixtures(("kotoba_v2_b64_bf16",))
     if not a.skip_large and a.only in (None, "kotoba"):
         cases = [("tone", 1), ("dummy", 2)]
         modes = [{"name": "greedy", "kw": dict(base, return_timestamps=False), "scores": True}]
