@@ -119,9 +119,9 @@ def parse(argv=None):
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--kernel-iters", type=int, default=20)
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="extra measurement (not the headline value): this many bs-32 batches decoding at once, one "
-                         "host thread and stream each over engine lanes sharing the weights; 1 = skip")
+    ap.add_argument("--inflight", default="2,3",
+                    help="extra measurements (not the headline value): comma list of how many bs-32 batches decode at "
+                         "once, one host thread and stream each over engine lanes sharing the weights; '' = skip")
     ap.add_argument("--stub", action="store_true",
                     help="no GPU work: each rank times a trivial host step (tests the launcher, barriers, "
                          "max-over-ranks timing and the ids gather on the CPU; with KW_BENCH_BACKEND=gloo)")
@@ -323,7 +323,8 @@ def main(argv=None):
                 "ms_per_batch": dt_ / n_batches * 1e3,
                 "note": "NOT the headline value: batches of 32 decoded concurrently, each generate() call at bs 32"}
 
-    inflight = inflight_rate(a.inflight, max(2 * a.inflight, a.steps)) if a.inflight > 1 and world == 1 else None
+    lanes_list = [int(x) for x in str(a.inflight).split(",") if x.strip() and int(x) > 1]
+    inflight = [inflight_rate(n, max(2 * n, a.steps)) for n in lanes_list] if lanes_list and world == 1 else None
 
     # ---- per-kernel measurements (HIP events on the launching stream, after the timed region) ----
     eng = model.engine

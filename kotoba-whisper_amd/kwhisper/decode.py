@@ -455,7 +455,7 @@ class DecodeSession:
             if self._poll(pinned, events, rep, lag, self.n_unfinished):
                 break
             rep += 1
-        torch.cuda.synchronize(dev)
+        torch.cuda.current_stream(dev).synchronize()  # (this stream only: other lanes keep running)
         self.check_handoffs()
         L_now = int(self.cur_len.item())
         ids = self.ids[:, :L_now].cpu().numpy()
@@ -571,7 +571,7 @@ class DecodeSession:
             if self._poll(pinned, events, n - 1, check_every, st["go"]):
                 break
             n += 1
-        torch.cuda.synchronize(dev)
+        torch.cuda.current_stream(dev).synchronize()  # (this stream only: other lanes keep running)
         self.check_handoffs()
         fin_len = st["fin_len"][:, 0].cpu().numpy()
         out = st["fin_seq"][:, 0].cpu().numpy()

@@ -354,10 +354,19 @@ def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, com
             run_step(si, decoders[si])
         errs: List[BaseException] = []
 
+        import contextlib
+
+        # each lane on its own stream of this rank's device (on one shared stream the lanes would serialise; a new
+        # thread's current device is 0, the stream context sets it)
+        streams = [torch.cuda.Stream(device=torch.cuda.current_device()) for _ in range(n)] \
+            if torch.cuda.is_available() else [None] * n
+
         def lane_work(i):
             try:
-                for si in range(i + n, n_steps, n):
-                    run_step(si, decoders[i])
+                ctx = torch.cuda.stream(streams[i]) if streams[i] is not None else contextlib.nullcontext()
+                with ctx:
+                    for si in range(i + n, n_steps, n):
+                        run_step(si, decoders[i])
             except BaseException as e:  # re-raised on the calling thread
                 errs.append(e)
 
