@@ -76,6 +76,7 @@ class DecodeSession:
         self.samp_ws = torch.zeros((ops.greedy_step_workspace_bytes(R) + 3) // 4, device=dev, dtype=torch.float32)
         self._greedy_cfg = {}
         self._pinned = None
+        self.last_steps = 0
         if enc is not None:
             self.set_encoder_output(enc)
 
@@ -455,6 +456,7 @@ class DecodeSession:
             if self._poll(pinned, events, rep, lag, self.n_unfinished):
                 break
             rep += 1
+        self.last_steps = done  # steps issued (tests: the stop check fires within lag steps of the last EOS)
         torch.cuda.current_stream(dev).synchronize()  # (this stream only: other lanes keep running)
         self.check_handoffs()
         L_now = int(self.cur_len.item())

@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import csv
 import os
+import threading
 from typing import Callable, Iterable, List, Optional, Sequence
 
 import numpy as np
@@ -347,8 +348,6 @@ def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, com
             run_step(si, decoders[0])
     else:  # lanes: step si on lane si % n (one host thread each); lane i's first step runs alone first, so every
         # lane's graphs are captured before the threads overlap
-        import threading
-
         n = len(decoders)
         for si in range(min(n, n_steps)):
             run_step(si, decoders[si])
@@ -438,6 +437,13 @@ def gather_matrices(mats: Sequence[np.ndarray], n_slots: int, pad: int, device=N
 
 
 _GATHER = {"round": _label_loop, "end": _label_loop_deferred}
+_STEP = threading.local()
+
+
+def step_model():
+    """Inside an ``on_step`` callback: the model handle (the caller's model or one of its lanes) that decoded the
+    step just reported -- with ``lanes`` > 1 the steps run on lane threads, each lane's ``stats`` its own."""
+    return getattr(_STEP, "model", None)
 
 
 def _lane_models(model, lanes: int, gather: str):
@@ -493,6 +499,7 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
 
     def decoder(m):
         def decode(feats):
+            _STEP.model = m  # (step_model(): the lane handle whose stats an on_step callback should read)
             ids = m.generate(feats, **gen_kwargs)
             return [_with_prompt(ids, prompt) if prompt else ids]
 

@@ -431,6 +431,43 @@ def test_steps_per_replay_tokens_identical(tiny16, ts, eos):
     assert torch.equal(out[1], out[2]) and torch.equal(out[1], out[3])
 
 
+@pytest.mark.parametrize("k", [1, 2, 3])
+def test_stop_check_fires_after_last_eos(tiny16, k):
+    """The host stop check reads the unfinished-row count a few replays behind, from a pinned slot that first gets
+    a -1 sentinel (r03al).  A slot read before its copy lands would never stop the loop (silently decoding to
+    max_length): once every row has emitted EOS the loop must stop within its lag (check_every steps) plus one
+    replay.  EOS is chosen from a first run as a token every row emits, so every row finishes early."""
+    g = torch.Generator(device="cuda").manual_seed(13)
+    feats = torch.randn(6, TINY.num_mel_bins, TINY.n_frames, device="cuda", generator=g) * 0.5
+    gen = generation_constants(TINY)
+    kw = dict(language="ja", task="transcribe", return_timestamps=False, max_length=120)
+    eng = tiny16.engine
+    try:
+        eng.steps_per_replay = k
+        ids = tiny16.generate(feats, generation_config=gen, **kw).cpu()
+        P = 4 if int(ids[0, 0]) == gen.decoder_start_token_id else 0  # (prompt kept in the output or not)
+        body = ids[:, P:]
+        first = {}  # token -> the latest step at which a row first emits it
+        for t in set(body[0].tolist()):
+            hits = [(row == t).nonzero() for row in body]
+            if all(len(h) for h in hits):
+                first[t] = max(int(h[0]) for h in hits)
+        if not first:
+            pytest.skip("no token common to every row")
+        eos, s = min(first.items(), key=lambda kv: kv[1])
+        if s + 1 + 4 + k >= 120 - P:
+            pytest.skip("rows finish too close to max_length")
+        gen2 = generation_constants(TINY)
+        gen2.eos_token_id = eos
+        out = tiny16.generate(feats, generation_config=gen2, **kw).cpu()
+        steps = tiny16._session(6).last_steps
+    finally:
+        eng.steps_per_replay = 2
+    assert out.shape[1] == P + s + 1, (out.shape, P, s)
+    # the loop issued at most the steps up to the last EOS, the lag (4 steps) and one more replay
+    assert s + 1 <= steps <= s + 1 + 4 + k, (steps, s, k)
+
+
 @pytest.mark.parametrize("block", ["kw_dec_qkv_self", "kw_dec_xq_cross"])
 def test_handoff_timeout_raises(gold, tiny16, block):
     """A fused decode block whose in-launch hand-off times out must fail the call, not return tokens (VERDICT r3

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 import torch
 
-from kwhisper.pseudo_label import gather_remainder, pseudo_label, shard_batches, write_transcription_csv
+from kwhisper.pseudo_label import gather_remainder, pseudo_label, shard_batches, step_model, write_transcription_csv
 
 PAD = 50256
 
@@ -418,10 +418,19 @@ def test_lanes_return_the_single_lane_predictions(n, bs, lanes):
     (and their order) equal the single-lane run's, and every batch is decoded exactly once."""
     ref = pseudo_label(_StubModel(), _features, n, batch_size=bs, pad_token_id=PAD, gather="end")
     m = _LaneStub()
-    got = pseudo_label(m, _features, n, batch_size=bs, pad_token_id=PAD, gather="end", lanes=lanes)
+    seen = {}  # step -> the handle step_model() names inside on_step (bench_configs reads that lane's stats)
+
+    def on_step(si, total):
+        seen[si] = step_model()
+
+    got = pseudo_label(m, _features, n, batch_size=bs, pad_token_id=PAD, gather="end", lanes=lanes, on_step=on_step)
     _same(got, ref)
     decoded = sorted(i for lane in m.lanes for b in lane.batches for i in b)
     want = sorted(i for b in shard_batches(n, bs, 1, 0) for i in b)
     assert decoded == want and len(m.lanes) == lanes
+    steps = shard_batches(n, bs, 1, 0)
+    assert sorted(seen) == list(range(len(steps)))
+    for si, h in seen.items():  # the handle that reported step si decoded its batch
+        assert list(steps[si]) in [list(b) for b in h.batches]
     with pytest.raises(ValueError, match="gather"):
         pseudo_label(_LaneStub(), _features, 3, batch_size=4, pad_token_id=PAD, lanes=2)

@@ -51,7 +51,7 @@ def config4(a, world, rank, dev):
     from kwhisper.config import PRESETS
     from kwhisper.feature_extraction import WhisperFeatureExtractor
     from kwhisper.generation import KWhisperForConditionalGeneration
-    from kwhisper.pseudo_label import pseudo_label
+    from kwhisper.pseudo_label import pseudo_label, step_model
     from kwhisper.synthetic import synthetic_state_dict_torch
 
     shape = PRESETS["large-v3"]
@@ -82,11 +82,11 @@ def config4(a, world, rank, dev):
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    stamps, passes = [], []
+    stamps, passes = {}, {}  # by step (with lanes the steps complete on lane threads, out of order)
 
     def on_step(si, total):  # after each batch's tokens reached the host (and, gather="round", the gather)
-        stamps.append(time.perf_counter())
-        passes.append(int(model.stats.get("passes", 0)))
+        stamps[si] = time.perf_counter()
+        passes[si] = int((step_model() or model).stats.get("passes", 0))
 
     t0 = time.perf_counter()
     ids, preds = pseudo_label(model, features, n, batch_size=a.batch, gen_kwargs=gen_kw, gather=a.gather,
@@ -97,7 +97,8 @@ def config4(a, world, rank, dev):
         dist.barrier()
     dt = time.perf_counter() - t0
     assert ids == list(range(n))
-    batch_s = np.diff([t0] + stamps)
+    # per-batch seconds: completion-to-completion in step order (lanes overlap batches: no projection then)
+    batch_s = np.diff([t0] + [stamps[si] for si in sorted(stamps)])
     return {"metric": "audio-seconds/sec pseudo-labelling (real durations)", "value": float(durs.sum()) / dt,
             "unit": "audio-s/s", "padded_30s_value": n * 30.0 / dt, "n_gpus": world, "clips": n,
             "audio_seconds": float(durs.sum()), "seconds": dt, "higher_is_better": True, "scaling": "strong",
@@ -106,7 +107,7 @@ def config4(a, world, rank, dev):
                        "per_gpu_batch": a.batch, "max_length": a.max_length, "parallelism": f"dp{world}",
                        "gather": a.gather, "lanes": a.lanes,
                        "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))},
-            "batch_seconds": [round(float(x), 5) for x in batch_s], "batch_seek_passes": passes,
+            "batch_seconds": [round(float(x), 5) for x in batch_s], "batch_seek_passes": [passes[si] for si in sorted(passes)],
             "dp_projection": dp_projection(batch_s) if world == 1 and a.lanes == 1 else None}
 
 
