@@ -11,7 +11,6 @@ namespace {
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr int HD = 64;  // head_dim of every Whisper model
 
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 template <typename T>
 struct Row8 {
   u32x4 u[sizeof(T) == 2 ? 1 : 2];

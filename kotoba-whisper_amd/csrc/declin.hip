@@ -71,31 +71,24 @@ struct DecP {
   int xlds;  // stage the activation rows through LDS (single-round grids and split-K slices)
 };
 
-template <int KTM, int NCB, bool LNA, int EPI, typename TC>
-__global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
-  // blockIdx.z = 32-row chunk: a launch covers M rows as independent 32-row tiles (their workgroups
-  // run concurrently and the repeat weight reads of the later chunks hit the caches)
-  DecP p = p0;
-  if (ksn > 1) {  // K-split seam: each chunk has its own counters and partial slabs
-    p.cnt += blockIdx.z * gridDim.x;
-    p.slab += (int64_t)blockIdx.z * gridDim.x * ksn * (NCB * 512);
-  }
-  if (blockIdx.z) {
-    const int m0 = 32 * blockIdx.z;
-    p.M = min(32, p0.M - m0);
-    p.x += m0 * p0.ldx;
-    if (p.C) p.C = reinterpret_cast<char*>(p.C) + (int64_t)m0 * p0.ldc * (sizeof(TC));
-    if (p.h) p.h += m0 * p0.ldh;
-    if (p.hb) p.hb += m0 * p0.ldh;
-  } else {
-    p.M = min(32, p0.M);
-  }
+// The fused MLP's fc1 hand-off (dec_mlp_kernel below): instead of storing its bf16 GELU tile to C, a PUB
+// workgroup (NCB = 2: its 32 columns are k-tile cg of fc2's K) writes the tile to hx in the MFMA A-fragment
+// layout fc2's waves load ([k-tile][row half][64 lanes][16 B]) by 16-B sc1 (write-through) stores, drains them and
+// sets flags[cg] (MI355X_MICROARCH visibility table, first row: sc1 stores, one lane's agent-scope flag, sc1 loads).
+struct MlpPub {
+  char* hx;
+  int* flags;
+  int* fault;  // test hook: nonzero -> workgroup 0 skips its flag once (kw_dec_mlp_status_offset)
+};
+
+template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool PUB>
+__device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int cg, const int ks, const int nw,
+                                                const MlpPub& pub) {
   __shared__ f32x4 red[MAXW][NCB][2][64];
   __shared__ float rpart[MAXW][32][2];  // LayerNorm: per-wave row (sum, sum of squares)
   __shared__ float rstat[32][2];     // LayerNorm: (mean, rstd) per row
   extern __shared__ __attribute__((aligned(16))) char xs[];  // activation image (x_lds_bytes)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
-  const int cg = blockIdx.x, ks = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nkt = p.K >> 5;
   const int nsl = ksn * nw, sl = ks * nw + wave;
   const int kt0 = (nkt * sl) / nsl, kt1 = (nkt * (sl + 1)) / nsl;  // <= KTM k-tiles (host-checked)
@@ -334,13 +327,227 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
         } else {
           if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
           if (n < p.scale_cols) v *= p.scale;
-          if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
+          if constexpr (PUB) {
+            // every row (rows >= M are clamped copies: fc2 discards them), row-major 32 x 32 tile in LDS
+            reinterpret_cast<bf16_t*>(xs)[m * 40 + c * 16 + (lane & 15)] = f2bf(v);
+          } else {
+            if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
+          }
         }
       }
     }
   }
+  if constexpr (PUB) {
+    // wave 0 alone: the tile back out in fragment order (row 16 hh + lane % 16, columns 8 (lane / 16) + 0..7),
+    // two 16-B write-through stores per lane, drained, then one lane sets this k-tile's flag
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx + (int64_t)cg * 2048, (short)0, 2048, 0x00020000);
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const u32x4 t = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(xs) + (16 * hh + (lane & 15)) * 40 +
+                                                      8 * (lane >> 4));
+      __builtin_amdgcn_raw_buffer_store_b128(t, rs, (hh * 64 + lane) * 16, 0, 16);  // aux 16 = sc1
+    }
+    const int fault = __hip_atomic_load(pub.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      if (cg == 0 && fault != 0)
+        __hip_atomic_store(pub.fault, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // drop this launch's flag once
+      else
+        __hip_atomic_store(pub.flags + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   KW_DEC_STAMP(4);
   KW_DEC_STAMP_FLUSH
+}
+
+template <int KTM, int NCB, bool LNA, int EPI, typename TC>
+__global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
+  // blockIdx.z = 32-row chunk: a launch covers M rows as independent 32-row tiles (their workgroups
+  // run concurrently and the repeat weight reads of the later chunks hit the caches)
+  DecP p = p0;
+  if (ksn > 1) {  // K-split seam: each chunk has its own counters and partial slabs
+    p.cnt += blockIdx.z * gridDim.x;
+    p.slab += (int64_t)blockIdx.z * gridDim.x * ksn * (NCB * 512);
+  }
+  if (blockIdx.z) {
+    const int m0 = 32 * blockIdx.z;
+    p.M = min(32, p0.M - m0);
+    p.x += m0 * p0.ldx;
+    if (p.C) p.C = reinterpret_cast<char*>(p.C) + (int64_t)m0 * p0.ldc * (sizeof(TC));
+    if (p.h) p.h += m0 * p0.ldh;
+    if (p.hb) p.hb += m0 * p0.ldh;
+  } else {
+    p.M = min(32, p0.M);
+  }
+  dec_linear_body<KTM, NCB, LNA, EPI, TC, false>(p, ksn, blockIdx.x, blockIdx.y, blockDim.x >> 6, MlpPub{});
+}
+
+// ---- fused decode MLP: fc1 (LayerNorm-fused, GELU) -> fc2 (+ residual) in ONE launch (kw_dec_mlp) ----
+// Workgroups [0, n1): fc1 exactly as dec_linear_kernel<5, 2, true, STORE, bf16> computes it (dec_linear_body), each
+// publishing its 32 columns -- one k-tile of fc2's K -- through MlpPub.  Workgroups [n1, n1 + N/16): one per 16
+// columns of fc2, each doing ALL of that column block's work of the two-launch plan's split-K fc2 (ks K-splits x nw2
+// waves = ks * nw2 slices of <= 5 k-tiles, spread over its 8 waves): every slice's weight fragments are in flight from
+// the start (they stream while fc1 runs: the split-K launch's weight round trip and the launch boundary leave the
+// chain), a slice waits only for the flags of its own k-tiles, loads their fragments by sc1 loads, and its MFMA
+// partial goes to LDS; wave 0 then sums the partials in the two-launch plan's order (waves of a K-split, then the
+// K-splits with the seam's zero terms) and applies the RESID epilogue -- h and hb bitwise those of the two
+// launches.  Every wait is on a workgroup dispatched earlier in the same launch (fc1 never waits), so the launch
+// cannot deadlock at any residency; the last fc2 workgroup through re-arms the flags.  A poll that outlasts
+// MLP_SPIN_LIMIT sets the status word and writes NaN rows (kw_dec_mlp_status_offset).
+constexpr int MLP_SLW = 5;               // fc2 slices per wave (<= 8 x 5 = 40 slices)
+constexpr int MLP_HDR = 1024;            // workspace ints before the fragment image: flags, done, status, fault
+constexpr int MLP_DONE = MLP_HDR - 4, MLP_STATUS = MLP_HDR - 3, MLP_FAULT = MLP_HDR - 2;
+constexpr int MLP_SPIN_LIMIT = 1 << 22;
+
+struct MlpArgs {
+  DecP f1, f2;  // fc1: LayerNorm-fused STORE (gelu, bf16, xlds); fc2: RESID (h, hb)
+  char* hx;     // fc1's output as fc2 A-fragments: [F / 32][2][64][16 B]
+  int* ws;      // MLP_HDR ints: flags[F / 32], done, status, fault
+  int n1;       // fc1 workgroups (= F / 32 k-tiles of fc2)
+  int ks2, nw2; // fc2's two-launch geometry (choose(d, F))
+};
+
+__device__ __forceinline__ bool mlp_wait(const int* flags, int kt0, int kt1, int lane, int* status) {
+  const bool mine = lane < kt1 - kt0;
+  const int* f = flags + kt0 + (mine ? lane : 0);
+  for (int it = 0;; ++it) {
+    const int v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_amdgcn_ballot_w64(mine && v == 0) == 0) return true;
+    if (it >= MLP_SPIN_LIMIT) {
+      if (lane == 0) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(KW_POLL_SLEEP);
+  }
+}
+
+__device__ __forceinline__ void mlp_fc2_role(const MlpArgs& a, const int cb) {
+  extern __shared__ __attribute__((aligned(16))) char xs[];
+  __shared__ int tmo;
+  f32x4(*part)[2][64] = reinterpret_cast<f32x4(*)[2][64]>(xs);  // [slice][row half][lane]
+  const DecP& p = a.f2;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nkt = p.K >> 5, ksn = a.ks2, nw2 = a.nw2, S = ksn * nw2;
+  const int M = p.M;
+  if (threadIdx.x == 0) tmo = 0;
+  // 1. every slice's weights in flight (non-temporal), then the epilogue operands (wave 0)
+  bf16x8 w[MLP_SLW][5];
+#pragma unroll
+  for (int j = 0; j < MLP_SLW; ++j) {
+    const int sl = wave + 8 * j;
+    if (sl < S) {
+      const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S, ktl = max(kt1 - 1, kt0);
+#pragma unroll
+      for (int u = 0; u < 5; ++u)
+        w[j][u] = __builtin_nontemporal_load(p.W + ((int64_t)cb * nkt + min(kt0 + u, ktl)) * 64 + lane);
+    }
+  }
+  const int n_e = min(cb * 16 + (lane & 15), p.N - 1);
+  float hold[2][4], ebias = 0.f;
+  if (wave == 0) {
+    ebias = p.bias ? p.bias[n_e] : 0.f;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) hold[hh][r] = p.h[(int64_t)min(16 * hh + 4 * (lane >> 4) + r, M - 1) * p.ldh + n_e];
+  }
+  // 2. per slice: its k-tiles' flags, their A fragments (sc1: written in this launch by other CUs), MFMA -> LDS
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.hx, (short)0, nkt * 2048, 0x00020000);
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < MLP_SLW; ++j) {
+    const int sl = wave + 8 * j;
+    if (sl >= S) break;
+    const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S, ktl = max(kt1 - 1, kt0);
+    if (ok) ok = mlp_wait(a.ws, kt0, kt1, lane, a.ws + MLP_STATUS);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+    bf16x8 a0[5], a1[5];
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const int kt = min(kt0 + u, ktl);
+      a0[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 0) * 1024 + lane * 16, 0, 16));
+      a1[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 1) * 1024 + lane * 16, 0, 16));
+    }
+    f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
+#pragma unroll
+    for (int u = 0; u < 5; ++u)
+      if (kt0 + u < kt1) {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], w[j][u], c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[j][u], c1, 0, 0, 0);
+      }
+    part[sl][0][lane] = c0;
+    part[sl][1][lane] = c1;
+  }
+  if (!ok && lane == 0) tmo = 1;
+  __syncthreads();
+  if (wave != 0) return;
+  // every wave of this workgroup is past its polls: the last fc2 workgroup through re-arms the flags
+  int last = 0;
+  if (lane == 0) last = __hip_atomic_fetch_add(a.ws + MLP_DONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                        (int)gridDim.x - a.n1 - 1;
+  if (__shfl(last, 0, 64)) {
+    for (int i = lane; i < nkt; i += 64) __hip_atomic_store(a.ws + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) __hip_atomic_store(a.ws + MLP_DONE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // 3. the two-launch plan's sums: a K-split's waves in order (dec_linear_body step 4), then the seam's K-splits in
+  //    order with its zero terms up to KSMAX (step 5)
+  f32x4 c0, c1;
+  if (ksn == 1) {
+    c0 = part[0][0][lane];
+    c1 = part[0][1][lane];
+    for (int w2 = 1; w2 < nw2; ++w2) {
+      c0 += part[w2][0][lane];
+      c1 += part[w2][1][lane];
+    }
+  } else {
+    for (int q = 0; q < KSMAX; ++q) {
+      f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
+      if (q < ksn) {
+        s0 = part[q * nw2][0][lane];
+        s1 = part[q * nw2][1][lane];
+        for (int w2 = 1; w2 < nw2; ++w2) {
+          s0 += part[q * nw2 + w2][0][lane];
+          s1 += part[q * nw2 + w2][1][lane];
+        }
+      }
+      if (q == 0) {
+        c0 = s0;
+        c1 = s1;
+      } else {
+        c0 += s0;
+        c1 += s1;
+      }
+    }
+  }
+  // 4. RESID epilogue (dec_linear_body step 6)
+  const bool bad = tmo != 0;
+  const int n = cb * 16 + (lane & 15);
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * hh + 4 * (lane >> 4) + r;
+      float v = hh ? c1[r] : c0[r];
+      v += ebias;
+      v += hold[hh][r];
+      if (bad) v = __builtin_nanf("");
+      if (n < p.N && m < M) {
+        p.h[(int64_t)m * p.ldh + n] = v;
+        p.hb[(int64_t)m * p.ldh + n] = f2bf(v);
+      }
+    }
+}
+
+__global__ __launch_bounds__(512) void dec_mlp_kernel(MlpArgs a) {
+  if ((int)blockIdx.x < a.n1) {
+    const MlpPub pub{a.hx, a.ws, a.ws + MLP_FAULT};
+    dec_linear_body<5, 2, true, KW_EPI_STORE, bf16_t, true>(a.f1, 1, blockIdx.x, 0, 8, pub);
+  } else {
+    mlp_fc2_role(a, blockIdx.x - a.n1);
+  }
 }
 
 // More than 32 rows without a K split (prefill positions, beam rows): each workgroup keeps its
@@ -1051,4 +1258,95 @@ extern "C" int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed,
                      (bf16_t*)packed);
   KW_CHECK_LAUNCH();
   return KW_OK;
+}
+
+// ---- kw_dec_mlp (dec_mlp_kernel): fc1 -> fc2 of a greedy decode step in one launch ----
+namespace {
+
+// The two-launch plan's geometries, and whether the fused kernel reproduces them: fc1 as 8 waves x 5 k-tiles with
+// 2 column blocks per workgroup (one k-tile of fc2 per workgroup), fc2 as K-split slices of <= 5 k-tiles that fit
+// 8 waves x MLP_SLW.
+bool mlp_geometry(int64_t M, int64_t d, int64_t F, Geo& g1, Geo& g2) {
+  if (M < 1 || M > 32 || d <= 0 || F <= 0 || d % 32 != 0 || F % 32 != 0) return false;
+  g1 = choose(F, d);
+  g2 = choose(d, F);
+  const int nkt1 = (int)(d / 32), nkt2 = (int)(F / 32);
+  if (g1.ncb != 2 || g1.ktm != 5 || g1.ks != 1 || g1.nw != 8 || (nkt1 + 7) / 8 > 5) return false;
+  if (g2.ncb != 1 || g2.ktm != 5 || g2.ks > KSMAX || g2.ks * g2.nw > 8 * MLP_SLW) return false;
+  if ((nkt2 + g2.ks * g2.nw - 1) / (g2.ks * g2.nw) > 5 || nkt2 > MLP_DONE) return false;
+  return true;
+}
+
+}  // namespace
+
+extern "C" int kw_dec_mlp_supported(int64_t M, int64_t d, int64_t F) {
+  Geo g1, g2;
+  return mlp_geometry(M, d, F, g1, g2) ? 1 : 0;
+}
+
+extern "C" size_t kw_dec_mlp_workspace(int64_t M, int64_t d, int64_t F) {
+  (void)M;
+  (void)d;
+  return (size_t)MLP_HDR * sizeof(int) + (size_t)(F / 32) * 2048;
+}
+
+extern "C" size_t kw_dec_mlp_status_offset(int64_t M, int64_t d, int64_t F) {
+  (void)M;
+  (void)d;
+  (void)F;
+  return (size_t)MLP_STATUS * sizeof(int);
+}
+
+extern "C" int kw_dec_mlp(const kw_dec_mlp_args* a, kw_stream_t stream) {
+  if (!a || !a->x || !a->fc1_w || !a->fc1_colsum || !a->fc2_w || !a->h || !a->hb || !a->workspace)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_mlp: null pointer");
+  Geo g1, g2;
+  if (!mlp_geometry(a->M, a->d, a->F, g1, g2))
+    return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_mlp: shape not covered (kw_dec_mlp_supported)");
+  if (a->ldx < a->d || a->ldx % 8 != 0 || (uintptr_t)a->x % 16 != 0 || a->ldh < a->d)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_mlp: ldx >= d (multiple of 8, x 16-B aligned), ldh >= d");
+  if (a->ws_bytes < kw_dec_mlp_workspace(a->M, a->d, a->F) || (uintptr_t)a->workspace % 16 != 0)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_mlp: needs a zero-filled, 16-B aligned workspace of kw_dec_mlp_workspace()");
+  MlpArgs m{};
+  DecP& p1 = m.f1;
+  p1.x = reinterpret_cast<const bf16_t*>(a->x);
+  p1.ldx = a->ldx;
+  p1.ln = 1;
+  p1.ln_eps = a->ln_eps;
+  p1.ln_colsum = a->fc1_colsum;
+  p1.W = reinterpret_cast<const bf16x8*>(a->fc1_w);
+  p1.bias = a->fc1_bias;
+  p1.gelu = 1;
+  p1.scale = 1.f;
+  p1.scale_cols = 0;
+  p1.M = (int)a->M;
+  p1.N = (int)a->F;
+  p1.K = (int)a->d;
+  p1.xlds = use_xlds(a->F, g1) ? 1 : 0;
+  DecP& p2 = m.f2;
+  p2.W = reinterpret_cast<const bf16x8*>(a->fc2_w);
+  p2.bias = a->fc2_bias;
+  p2.h = a->h;
+  p2.hb = reinterpret_cast<bf16_t*>(a->hb);
+  p2.ldh = a->ldh;
+  p2.M = (int)a->M;
+  p2.N = (int)a->d;
+  p2.K = (int)a->F;
+  m.ws = reinterpret_cast<int*>(a->workspace);
+  m.hx = reinterpret_cast<char*>(a->workspace) + MLP_HDR * sizeof(int);
+  m.n1 = (int)(a->F / 32);
+  m.ks2 = g2.ks;
+  m.nw2 = g2.nw;
+  const size_t shm = std::max(x_lds_bytes_for((int)(a->d / 32), 1, p1.xlds != 0), (size_t)g2.ks * g2.nw * 2048);
+  static size_t attr = 0;
+  if (shm > attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dec_mlp_kernel),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return kw_set_error(e);
+    attr = shm;
+  }
+  const unsigned grid = (unsigned)(m.n1 + (a->d + 15) / 16);
+  hipLaunchKernelGGL(dec_mlp_kernel, dim3(grid), dim3(512), shm, (hipStream_t)stream, m);
+  const hipError_t e = hipGetLastError();
+  return e == hipSuccess ? KW_OK : kw_set_error(e);
 }

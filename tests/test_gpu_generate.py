@@ -463,6 +463,7 @@ def test_stop_check_fires_after_last_eos(tiny16, k):
         steps = tiny16._session(6).last_steps
     finally:
         eng.steps_per_replay = 2
+    print(f"k {k}: P {P} eos {eos} last EOS at body index {s}; out {tuple(out.shape)}; steps issued {steps}")
     assert out.shape[1] == P + s + 1, (out.shape, P, s)
     # the loop issued at most the steps up to the last EOS, the lag (4 steps) and one more replay
     assert s + 1 <= steps <= s + 1 + 4 + k, (steps, s, k)
