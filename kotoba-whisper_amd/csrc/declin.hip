@@ -426,13 +426,12 @@ __device__ __forceinline__ bool mlp_wait(const int* flags, int kt0, int kt1, int
 
 __device__ __forceinline__ void mlp_fc2_role(const MlpArgs& a, const int cb) {
   extern __shared__ __attribute__((aligned(16))) char xs[];
-  __shared__ int tmo;
+  __shared__ int tmo[MAXW];  // per wave: a poll of this wave timed out
   f32x4(*part)[2][64] = reinterpret_cast<f32x4(*)[2][64]>(xs);  // [slice][row half][lane]
   const DecP& p = a.f2;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nkt = p.K >> 5, ksn = a.ks2, nw2 = a.nw2, S = ksn * nw2;
   const int M = p.M;
-  if (threadIdx.x == 0) tmo = 0;
   // 1. every slice's weights in flight (non-temporal), then the epilogue operands (wave 0)
   bf16x8 w[MLP_SLW][5];
 #pragma unroll
@@ -481,7 +480,7 @@ __device__ __forceinline__ void mlp_fc2_role(const MlpArgs& a, const int cb) {
     part[sl][0][lane] = c0;
     part[sl][1][lane] = c1;
   }
-  if (!ok && lane == 0) tmo = 1;
+  if (lane == 0) tmo[wave] = ok ? 0 : 1;
   __syncthreads();
   if (wave != 0) return;
   // every wave of this workgroup is past its polls: the last fc2 workgroup through re-arms the flags
@@ -523,7 +522,8 @@ __device__ __forceinline__ void mlp_fc2_role(const MlpArgs& a, const int cb) {
     }
   }
   // 4. RESID epilogue (dec_linear_body step 6)
-  const bool bad = tmo != 0;
+  bool bad = false;
+  for (int w2 = 0; w2 < MAXW; ++w2) bad |= tmo[w2] != 0;
   const int n = cb * 16 + (lane & 15);
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh)
