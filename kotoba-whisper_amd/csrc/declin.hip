@@ -410,9 +410,10 @@ struct MlpArgs {
   int ks2, nw2; // fc2's two-launch geometry (choose(d, F))
 };
 
-__device__ __forceinline__ bool mlp_wait(const int* flags, int kt0, int kt1, int lane, int* status) {
-  const bool mine = lane < kt1 - kt0;
-  const int* f = flags + kt0 + (mine ? lane : 0);
+// One wave polls up to 64 flags at once: lane l the flag fidx (< 0: none).
+__device__ __forceinline__ bool mlp_wait(const int* flags, int fidx, int lane, int* status) {
+  const bool mine = fidx >= 0;
+  const int* f = flags + (mine ? fidx : 0);
   for (int it = 0;; ++it) {
     const int v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (__builtin_amdgcn_ballot_w64(mine && v == 0) == 0) return true;
@@ -453,29 +454,49 @@ __device__ __forceinline__ void mlp_fc2_role(const MlpArgs& a, const int cb) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) hold[hh][r] = p.h[(int64_t)min(16 * hh + 4 * (lane >> 4) + r, M - 1) * p.ldh + n_e];
   }
-  // 2. per slice: its k-tiles' flags, their A fragments (sc1: written in this launch by other CUs), MFMA -> LDS
+  // 2. ONE poll for the flags of every k-tile of this wave's slices (fc1's workgroups finish together: a poll per
+  //    slice paid a round trip each, r04i), then the slices' A fragments (sc1: written in this launch by other CUs)
+  //    double-buffered, slice j + 1's loads in flight under slice j's MFMAs; partials -> LDS
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.hx, (short)0, nkt * 2048, 0x00020000);
-  bool ok = true;
+  int fidx = -1;
+  {
+    int cum = 0;
+#pragma unroll
+    for (int j = 0; j < MLP_SLW; ++j) {
+      const int sl = wave + 8 * j;
+      if (sl < S) {
+        const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S;
+        if (lane >= cum && lane < cum + (kt1 - kt0)) fidx = kt0 + lane - cum;
+        cum += kt1 - kt0;
+      }
+    }
+  }
+  const bool ok = mlp_wait(a.ws, fidx, lane, a.ws + MLP_STATUS);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+  bf16x8 av[2][2][5];  // [buffer][row half][k-tile]
+  auto load = [&](int j, int buf) {
+    const int sl = wave + 8 * j;
+    const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S, ktl = max(kt1 - 1, kt0);
+#pragma unroll
+    for (int u = 0; u < 5; ++u) {
+      const int kt = min(kt0 + u, ktl);
+      av[buf][0][u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 0) * 1024 + lane * 16, 0, 16));
+      av[buf][1][u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 1) * 1024 + lane * 16, 0, 16));
+    }
+  };
+  if (wave < S) load(0, 0);
 #pragma unroll
   for (int j = 0; j < MLP_SLW; ++j) {
     const int sl = wave + 8 * j;
     if (sl >= S) break;
-    const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S, ktl = max(kt1 - 1, kt0);
-    if (ok) ok = mlp_wait(a.ws, kt0, kt1, lane, a.ws + MLP_STATUS);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
-    bf16x8 a0[5], a1[5];
-#pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int kt = min(kt0 + u, ktl);
-      a0[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 0) * 1024 + lane * 16, 0, 16));
-      a1[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 1) * 1024 + lane * 16, 0, 16));
-    }
+    if (sl + 8 < S) load(j + 1, (j + 1) & 1);
+    const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S;
     f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
     for (int u = 0; u < 5; ++u)
       if (kt0 + u < kt1) {
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], w[j][u], c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[j][u], c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[j & 1][0][u], w[j][u], c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[j & 1][1][u], w[j][u], c1, 0, 0, 0);
       }
     part[sl][0][lane] = c0;
     part[sl][1][lane] = c1;

@@ -454,7 +454,9 @@ def test_stop_check_fires_after_last_eos(tiny16, k):
                 first[t] = max(int(h[0]) for h in hits)
         if not first:
             pytest.skip("no token common to every row")
-        eos, s = min(first.items(), key=lambda kv: kv[1])
+        # prefer an EOS every row reaches after a few steps (the stop then fires mid-loop, not right after prefill)
+        late = {t: v for t, v in first.items() if v >= 4}
+        eos, s = min((late or first).items(), key=lambda kv: kv[1])
         if s + 1 + 4 + k >= 120 - P:
             pytest.skip("rows finish too close to max_length")
         gen2 = generation_constants(TINY)
@@ -464,7 +466,7 @@ def test_stop_check_fires_after_last_eos(tiny16, k):
     finally:
         eng.steps_per_replay = 2
     print(f"k {k}: P {P} eos {eos} last EOS at body index {s}; out {tuple(out.shape)}; steps issued {steps}")
-    assert out.shape[1] == P + s + 1, (out.shape, P, s)
+    assert out.shape[1] == P + s, (out.shape, P, s)  # the last row's EOS ends its segment and is stripped (HF)
     # the loop issued at most the steps up to the last EOS, the lag (4 steps) and one more replay
     assert s + 1 <= steps <= s + 1 + 4 + k, (steps, s, k)
 
