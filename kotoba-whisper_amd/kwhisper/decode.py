@@ -71,7 +71,7 @@ class DecodeSession:
                                  dtype=torch.float32) if self.xc_ok else None
         # fused feed-forward block (kw_dec_mlp): greedy rows, the large-v3 / kotoba-whisper FFN shape; h and hb
         # bitwise the two-launch plan's
-        self.mlp_ok = (eng.packed and beams == 1 and getattr(eng, "fuse_mlp", True) and R <= 32
+        self.mlp_ok = (eng.packed and beams == 1 and getattr(eng, "fuse_mlp", False) and R <= 32
                        and ops.mlp_supported(R, d, s.decoder_ffn_dim))
         self.mlp_ws = torch.zeros(((ops.mlp_workspace_bytes(R, d, s.decoder_ffn_dim) + 3) // 4,), device=dev,
                                   dtype=torch.float32) if self.mlp_ok else None
