@@ -220,7 +220,7 @@ class ASRPipeline:
 
     def __init__(self, model, feature_extractor=None, tokenizer=None, *, chunk_length_s: float = 0,
                  stride_length_s=None, batch_size: int = 1, generate_kwargs: Optional[dict] = None,
-                 return_timestamps=None, data_parallel: bool = True):
+                 return_timestamps=None, data_parallel: bool = True, lanes: int = 1):
         from .feature_extraction import WhisperFeatureExtractor
 
         self.model = model
@@ -235,6 +235,15 @@ class ASRPipeline:
         # with a torch.distributed process group: window batches round-robin over the ranks, one gather of the
         # token matrices at the end, every rank returns the full result (config 5 at W GPUs)
         self.data_parallel = bool(data_parallel)
+        # lanes > 1: that many window batches decode at once on model.lane() handles (shared weights), one host
+        # thread and stream each -- one batch's latency-bound decode chain beside another's HBM-bound
+        # cross-attention (kwhisper.pseudo_label lanes); the output is the same
+        if int(lanes) < 1:
+            raise ValueError("lanes must be >= 1")
+        if int(lanes) > 1 and not hasattr(model, "lane"):
+            raise ValueError("lanes > 1 needs a model with lane() (an independent handle on the same weights)")
+        self.lanes = int(lanes)
+        self._lane_models = None
         self.generation_config = self._pipeline_generation_config(model.generation_config)
 
     # the ASR pipeline's own generation defaults (TF/pipelines/automatic_speech_recognition.py:160-163)
@@ -351,6 +360,49 @@ class ASRPipeline:
             mask[i, : f["attention_mask"].shape[-1]] = f["attention_mask"][0]
         return feats, mask
 
+    def _decode_one(self, model, batch, gk):
+        feats, mask = self._batch_features([c["audio"] for _, c in batch])
+        out = model.generate(feats, attention_mask=mask, **gk)
+        ids = out["sequences"] if isinstance(out, dict) else out
+        return ids.cpu().numpy()
+
+    def _decode_batches(self, batches, gk):
+        """generate() over the window batches, in order: on the model alone, or (lanes > 1) batch j on lane j % n,
+        lane i's first batch alone first (its graphs captured before the threads overlap), then one thread and
+        stream per lane."""
+        n = min(self.lanes, max(1, len(batches)))
+        if n == 1:
+            return [self._decode_one(self.model, b, gk) for b in batches]
+        if self._lane_models is None or len(self._lane_models) < n:
+            self._lane_models = [self.model] + [self.model.lane() for _ in range(n - 1)]
+        models = self._lane_models[:n]
+        local = [None] * len(batches)
+        for j in range(n):
+            local[j] = self._decode_one(models[j], batches[j], gk)
+        import contextlib
+        import threading
+
+        streams = [torch.cuda.Stream(device=torch.cuda.current_device()) for _ in range(n)] \
+            if torch.cuda.is_available() else [None] * n
+        errs = []
+
+        def work(i):
+            try:
+                with torch.cuda.stream(streams[i]) if streams[i] is not None else contextlib.nullcontext():
+                    for j in range(i + n, len(batches), n):
+                        local[j] = self._decode_one(models[i], batches[j], gk)
+            except BaseException as e:  # re-raised on the calling thread
+                errs.append(e)
+
+        threads = [threading.Thread(target=work, args=(i,)) for i in range(n)]
+        for th in threads:
+            th.start()
+        for th in threads:
+            th.join()
+        if errs:
+            raise errs[0]
+        return local
+
     # ---- forward (:483-560) + postprocess (:600-710) -----------------------------------------------------
     def __call__(self, inputs, *, chunk_length_s=None, stride_length_s=None, return_timestamps=None,
                  return_language=None, generate_kwargs: Optional[dict] = None, batch_size: Optional[int] = None,
@@ -384,13 +436,7 @@ class ASRPipeline:
         dist = _dist() if self.data_parallel else None
         world, rank = (dist.get_world_size(), dist.get_rank()) if dist is not None else (1, 0)
         mine = starts[rank::world]  # data parallel: window batch j on rank j % W, no collective until the end
-        local = []
-        for b0 in mine:
-            batch = flat[b0: b0 + bs]
-            feats, mask = self._batch_features([c["audio"] for _, c in batch])
-            out = self.model.generate(feats, attention_mask=mask, **gk)
-            ids = out["sequences"] if isinstance(out, dict) else out
-            local.append(ids.cpu().numpy())
+        local = self._decode_batches([flat[b0: b0 + bs] for b0 in mine], gk)
         if dist is not None:  # one exchange: every rank's window batches as generate() returned them
             from .pseudo_label import gather_matrices
 

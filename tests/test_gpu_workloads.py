@@ -326,6 +326,27 @@ def test_config5_pipeline_kotoba_bf16_runs(gold):
     _free()
 
 
+def test_config5_pipeline_lanes_equal_one_lane(gold):
+    """ASRPipeline(lanes=2) on the bf16 kotoba-v2 engine (beam 5 + timestamps, window batches of 2 so that lanes
+    overlap): two window batches decode at once on model.lane() handles from two host threads, each on its own
+    stream; the merged output is identical to the one-lane run's (every beam graph per lane, stream-local syncs)."""
+    from kwhisper.pipeline import ASRPipeline
+
+    g = gold("pipeline_kotoba_v2_fp32")
+    m16 = _model(KOTOBA_V2, torch.bfloat16)
+    gk = json.loads(str(g["generate_kwargs"]))
+    clips = [{"array": clip_audio(c), "sampling_rate": 16000} for c in g["clips"]] * 2
+    out = {}
+    for lanes in (1, 2):
+        pipe = ASRPipeline(m16, tokenizer=StubTok(generation_constants(KOTOBA_V2)), chunk_length_s=15, batch_size=2,
+                           generate_kwargs=gk, lanes=lanes)
+        out[lanes] = jsonable(pipe(clips, return_timestamps=True))
+    print(f"\nconfig5 pipeline lanes: {len(clips)} clips, outputs equal {out[1] == out[2]}")
+    assert out[1] == out[2]
+    del m16
+    _free()
+
+
 @pytest.fixture(scope="module")
 def c5_b64(gold, kotoba32):
     """Config 5 at its BASELINE batch through ASRPipeline on the fp32 engine: 22 of tools/bench_configs.py's 30 s

@@ -281,3 +281,37 @@ def test_pipeline_data_parallel_gloo_matches_single_process(tmp_path, world):
         assert z["res"] == want
         calls.append(z["calls"])
     assert sum(calls) == m1.calls and max(calls) - min(calls) <= 1
+
+
+class _LaneASRModel(_StubASRModel):
+    """A stub with lane(): every handle counts its own generate() calls."""
+
+    def __init__(self, handles=None):
+        super().__init__()
+        self.handles = handles if handles is not None else [self]
+
+    def lane(self):
+        other = _LaneASRModel(self.handles)
+        self.handles.append(other)
+        return other
+
+
+@pytest.mark.parametrize("lanes", [2, 3])
+def test_pipeline_lanes_match_one_lane(lanes):
+    """ASRPipeline(lanes=n): window batches decode on n model handles from n host threads; the merged output equals
+    the one-lane run's, every batch is decoded exactly once, and a second call reuses the same handles."""
+    import json
+
+    from kwhisper.pipeline import ASRPipeline
+
+    enc = lambda r: json.loads(json.dumps(r, default=lambda x: x.tolist() if hasattr(x, "tolist") else x))  # noqa: E731
+    m1 = _StubASRModel()
+    want = enc(ASRPipeline(m1, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2)(_dp_clips()))
+    m = _LaneASRModel()
+    pipe = ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2, lanes=lanes)
+    for _ in range(2):
+        assert enc(pipe(_dp_clips())) == want
+    assert len(m.handles) == lanes
+    assert sum(h.calls for h in m.handles) == 2 * m1.calls
+    with pytest.raises(ValueError, match="lane"):
+        ASRPipeline(_StubASRModel(), feature_extractor=_StubFE(), lanes=2)

@@ -140,12 +140,13 @@ def config5(a, world, rank, dev):
     del sd
     # W > 1: the pipeline's window batches go round-robin over the ranks (ASRPipeline.data_parallel), one
     # gather of the token matrices at the end; every rank merges the full result
-    pipe = ASRPipeline(model, chunk_length_s=15, batch_size=a.batch,
+    pipe = ASRPipeline(model, chunk_length_s=15, batch_size=a.batch, lanes=a.lanes,
                        generate_kwargs=dict(language="ja", task="transcribe", num_beams=5, max_length=a.max_length))
     clips = [{"array": clip_audio(i, 30.0), "sampling_rate": SR} for i in range(a.clips)]
-    warm = ASRPipeline(model, chunk_length_s=15, batch_size=a.batch, data_parallel=False,
-                       generate_kwargs=dict(language="ja", task="transcribe", num_beams=5, max_length=a.max_length))
-    warm(clips[: max(1, a.batch // 3)], return_timestamps=True)  # warm-up (graph capture), no collective
+    # warm-up (graph capture on every lane), no collective: one window batch per lane (3 windows per 30 s clip)
+    pipe.data_parallel = False
+    pipe(clips[: max(1, a.batch // 3) * a.lanes], return_timestamps=True)
+    pipe.data_parallel = True
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -165,6 +166,7 @@ def config5(a, world, rank, dev):
             "data": "synthetic (run_speed_eval.py noise audio, random-init kotoba-whisper-v2.0 layout)",
             "config": {"workload": "config 5: kotoba-v2.0 (32 enc / 2 dec), beam 5 + timestamps, chunk_length_s 15",
                        "batch_windows": a.batch, "max_length": a.max_length, "parallelism": f"dp{world}",
+                       "lanes": a.lanes,
                        "tokens_per_clip_mean": float(np.mean([len(o["tokens"]) for o in out]))}}
 
 
@@ -178,7 +180,8 @@ def main():
     ap.add_argument("--gather", choices=("round", "end"), default="end",
                     help="config 4: the reference's per-batch gather (round) or one exchange at the end")
     ap.add_argument("--lanes", type=int, default=1,
-                    help="config 4: batches of --batch in flight per GPU (pseudo_label lanes; needs --gather end)")
+                    help="batches of --batch in flight per GPU (config 4: pseudo_label lanes, needs --gather end; "
+                    "config 5: ASRPipeline lanes)")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
