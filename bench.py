@@ -119,9 +119,11 @@ def parse(argv=None):
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--cpu-threads", type=int, default=None)
     ap.add_argument("--kernel-iters", type=int, default=20)
-    ap.add_argument("--inflight", default="2,3",
-                    help="extra measurements (not the headline value): comma list of how many bs-32 batches decode at "
-                         "once, one host thread and stream each over engine lanes sharing the weights; '' = skip")
+    ap.add_argument("--inflight", default="",
+                    help="extra measurements (not the headline value), e.g. '2,3': how many bs-32 batches decode at "
+                         "once, one host thread and stream each over engine lanes sharing the weights.  Off by default, "
+                         "so that the rocprofv3 trace of the default command times the kernels one batch at a time, as "
+                         "the roofline's live measurement does (profiles/r04k_bench.json holds a run with '2,3')")
     ap.add_argument("--stub", action="store_true",
                     help="no GPU work: each rank times a trivial host step (tests the launcher, barriers, "
                          "max-over-ranks timing and the ids gather on the CPU; with KW_BENCH_BACKEND=gloo)")

@@ -244,6 +244,7 @@ class ASRPipeline:
             raise ValueError("lanes > 1 needs a model with lane() (an independent handle on the same weights)")
         self.lanes = int(lanes)
         self._lane_models = None
+        self._lanes_run = set()  # lanes that have decoded a batch (their graphs captured) in an earlier call
         self.generation_config = self._pipeline_generation_config(model.generation_config)
 
     # the ASR pipeline's own generation defaults (TF/pipelines/automatic_speech_recognition.py:160-163)
@@ -368,7 +369,7 @@ class ASRPipeline:
 
     def _decode_batches(self, batches, gk):
         """generate() over the window batches, in order: on the model alone, or (lanes > 1) batch j on lane j % n,
-        lane i's first batch alone first (its graphs captured before the threads overlap), then one thread and
+        a lane's first batch ever alone first (its graphs captured before the threads overlap), then one thread and
         stream per lane."""
         n = min(self.lanes, max(1, len(batches)))
         if n == 1:
@@ -377,8 +378,14 @@ class ASRPipeline:
             self._lane_models = [self.model] + [self.model.lane() for _ in range(n - 1)]
         models = self._lane_models[:n]
         local = [None] * len(batches)
-        for j in range(n):
-            local[j] = self._decode_one(models[j], batches[j], gk)
+        first = {}  # lane -> its first batch index for the threads
+        for i in range(n):
+            if i in self._lanes_run:
+                first[i] = i
+            else:
+                local[i] = self._decode_one(models[i], batches[i], gk)
+                self._lanes_run.add(i)
+                first[i] = i + n
         import contextlib
         import threading
 
@@ -389,7 +396,7 @@ class ASRPipeline:
         def work(i):
             try:
                 with torch.cuda.stream(streams[i]) if streams[i] is not None else contextlib.nullcontext():
-                    for j in range(i + n, len(batches), n):
+                    for j in range(first[i], len(batches), n):
                         local[j] = self._decode_one(models[i], batches[j], gk)
             except BaseException as e:  # re-raised on the calling thread
                 errs.append(e)

@@ -145,7 +145,7 @@ def config5(a, world, rank, dev):
     clips = [{"array": clip_audio(i, 30.0), "sampling_rate": SR} for i in range(a.clips)]
     # warm-up (graph capture on every lane), no collective: one window batch per lane (3 windows per 30 s clip)
     pipe.data_parallel = False
-    pipe(clips[: max(1, a.batch // 3) * a.lanes], return_timestamps=True)
+    pipe(clips[: max(1, -(-a.batch * a.lanes // 3))], return_timestamps=True)  # >= one full batch per lane
     pipe.data_parallel = True
     torch.cuda.synchronize()
     if world > 1:
