@@ -69,6 +69,7 @@ struct DecP {
   float* slab;
   int* cnt;
   int xlds;  // stage the activation rows through LDS (single-round grids and split-K slices)
+  int zrows; // rows per grid z-chunk: 32, or 16 for narrow grids (row split, launch())
 };
 
 // The fused MLP's fc1 hand-off (dec_mlp_kernel below): instead of storing its bf16 GELU tile to C, a PUB
@@ -113,7 +114,9 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
   const int cpr = (wkt1 - wkt0) * 4, cprp = cpr + 1;
   const bool xlds = p.xlds;
   if (xlds) {
-    const int ninst = (32 * cprp + 63) / 64;
+    // <= 16 rows: only the pieces of rows 0..15 (the second row half's fragments then hold stale LDS, and its
+    // output rows -- all >= M -- are discarded; every row of an MFMA tile is independent of the others)
+    const int ninst = ((M <= 16 ? 16 : 32) * cprp + 63) / 64;
     const float inv = 1.0f / (float)cprp;
     const bf16_t* xk = p.x + (int64_t)wkt0 * 32;
     for (int j = wave; j < ninst; j += nw) {
@@ -373,14 +376,14 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
     p.slab += (int64_t)blockIdx.z * gridDim.x * ksn * (NCB * 512);
   }
   if (blockIdx.z) {
-    const int m0 = 32 * blockIdx.z;
-    p.M = min(32, p0.M - m0);
+    const int m0 = p0.zrows * blockIdx.z;
+    p.M = min(p0.zrows, p0.M - m0);
     p.x += m0 * p0.ldx;
     if (p.C) p.C = reinterpret_cast<char*>(p.C) + (int64_t)m0 * p0.ldc * (sizeof(TC));
     if (p.h) p.h += m0 * p0.ldh;
     if (p.hb) p.hb += m0 * p0.ldh;
   } else {
-    p.M = min(32, p0.M);
+    p.M = min(p0.zrows, p0.M);
   }
   dec_linear_body<KTM, NCB, LNA, EPI, TC, false>(p, ksn, blockIdx.x, blockIdx.y, blockDim.x >> 6, MlpPub{});
 }
@@ -1106,6 +1109,18 @@ Geo choose(int64_t N, int64_t K) {
 bool use_xlds(int64_t N, const Geo& g) { return g.ks > 1 || (N + 16 * g.ncb - 1) / (16 * g.ncb) <= 256; }
 size_t x_lds_bytes_for(int nkt, int ks, bool xlds) { return xlds ? x_lds_bytes((nkt + ks - 1) / ks) : 0; }
 
+bool row_split_on() {
+#ifdef KW_LAB_OVERRIDES
+  static const bool on = [] {  // lab builds: KW_DECLIN_ROWSPLIT=0 turns the row split off (A/B)
+    const char* e = getenv("KW_DECLIN_ROWSPLIT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+#else
+  return true;
+#endif
+}
+
 int device_cus() {
   static int ncu = 0;
   if (!ncu) {
@@ -1136,9 +1151,15 @@ hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = shm;
   }
-  const dim3 grid((unsigned)((p.N + 16 * NCB - 1) / (16 * NCB)), (unsigned)g.ks, (unsigned)((p.M + 31) / 32));
+  // row split: a grid of at most 128 column groups (the 1280-column linears: 80 workgroups on 256 CUs) runs its
+  // 17..32 rows as two 16-row chunks -- twice the workgroups, each staging half the activation rows (every output
+  // element is computed by the same operations: rows are independent)
+  DecP q = p;
+  const int ncg = (p.N + 16 * NCB - 1) / (16 * NCB);
+  q.zrows = (g.ks == 1 && p.M > 16 && p.M <= 32 && ncg <= 128 && row_split_on()) ? 16 : 32;
+  const dim3 grid((unsigned)ncg, (unsigned)g.ks, (unsigned)((p.M + q.zrows - 1) / q.zrows));
   const dim3 block((unsigned)(64 * g.nw));
-  hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, EPI, TC>), grid, block, shm, s, p, g.ks);
+  hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, EPI, TC>), grid, block, shm, s, q, g.ks);
   return hipGetLastError();
 }
 
