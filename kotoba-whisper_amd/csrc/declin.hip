@@ -82,7 +82,9 @@ struct MlpPub {
   int* fault;  // test hook: nonzero -> workgroup 0 skips its flag once (kw_dec_mlp_status_offset)
 };
 
-template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool PUB>
+// H2: the second 16-row half of the tile exists (false: a row-split chunk of <= 16 rows -- its a1 / c1 / LayerNorm
+// statistics are never loaded or computed, which frees the registers for two workgroups per CU)
+template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool PUB, bool H2 = true>
 __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int cg, const int ks, const int nw,
                                                 const MlpPub& pub) {
   __shared__ f32x4 red[MAXW][NCB][2][64];
@@ -146,7 +148,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
       for (int c = 0; c < NCB; ++c) {
         const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh)
+        for (int hh = 0; hh < (H2 ? 2 : 1); ++hh)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int m = min(16 * hh + 4 * (lane >> 4) + r, M - 1);
@@ -163,7 +165,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     for (int u = 0; u < KTM; ++u) {
       const int pos = (arow * cprp) + (min(kt0 + u, ktl) - wkt0) * 4 + (lane >> 4);
       a0[u] = *reinterpret_cast<const bf16x8*>(xs + pos * 16);
-      a1[u] = *reinterpret_cast<const bf16x8*>(xs + (pos + 16 * cprp) * 16);
+      if constexpr (H2) a1[u] = *reinterpret_cast<const bf16x8*>(xs + (pos + 16 * cprp) * 16);
     }
   } else {
     const int r0 = min(arow, M - 1), r1 = min(16 + arow, M - 1), akoff = 8 * (lane >> 4);
@@ -171,7 +173,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     for (int u = 0; u < KTM; ++u) {
       const int k = min(kt0 + u, ktl) * 32 + akoff;
       a0[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r0 * p.ldx + k);
-      a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
+      if constexpr (H2) a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
     }
   }
 
@@ -189,7 +191,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
 #pragma unroll
       for (int c = 0; c < NCB; ++c) {
         c0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], w[c][u], c0[c], 0, 0, 0);
-        c1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[c][u], c1[c], 0, 0, 0);
+        if constexpr (H2) c1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[c][u], c1[c], 0, 0, 0);
       }
     }
   }
@@ -207,22 +209,22 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     for (int u = 0; u < KTM; ++u)
       if (kt0 + u < kt1) {
         s0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], ones, s0, 0, 0, 0);
-        s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], ones, s1, 0, 0, 0);
+        if constexpr (H2) s1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], ones, s1, 0, 0, 0);
         q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], a0[u], q0, 0, 0, 0);
-        q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], a1[u], q1, 0, 0, 0);
+        if constexpr (H2) q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], a1[u], q1, 0, 0, 0);
       }
     // C layout: lane holds rows 4*(lane>>4)+i, column lane&15
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         rpart[wave][4 * (lane >> 4) + i][0] = s0[i];
-        rpart[wave][16 + 4 * (lane >> 4) + i][0] = s1[i];
+        if constexpr (H2) rpart[wave][16 + 4 * (lane >> 4) + i][0] = s1[i];
       }
     }
     const int di = (lane & 15) - 4 * (lane >> 4);  // diagonal element of this lane, if any
     if (di >= 0 && di < 4) {
       rpart[wave][lane & 15][1] = q0[di];
-      rpart[wave][16 + (lane & 15)][1] = q1[di];
+      if constexpr (H2) rpart[wave][16 + (lane & 15)][1] = q1[di];
     }
   }
 
@@ -232,7 +234,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
       red[wave][c][0][lane] = c0[c];
-      red[wave][c][1][lane] = c1[c];
+      if constexpr (H2) red[wave][c][1][lane] = c1[c];
     }
     __syncthreads();
     if (wave != 0) return;
@@ -240,7 +242,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
 #pragma unroll
       for (int c = 0; c < NCB; ++c) {
         c0[c] += red[w2][c][0][lane];
-        c1[c] += red[w2][c][1][lane];
+        if constexpr (H2) c1[c] += red[w2][c][1][lane];
       }
   }
   if constexpr (LNA) {  // wave 0: lane r < 32 sums row r's wave partials in wave order -> (mean, rstd)
@@ -313,7 +315,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     const float bn = ebias[c];
     const float cs = ecsum[c];
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
+    for (int hh = 0; hh < (H2 ? 2 : 1); ++hh) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 16 * hh + 4 * (lane >> 4) + r;
@@ -366,7 +368,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
   KW_DEC_STAMP_FLUSH
 }
 
-template <int KTM, int NCB, bool LNA, int EPI, typename TC>
+template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool H2 = true>
 __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
   // blockIdx.z = 32-row chunk: a launch covers M rows as independent 32-row tiles (their workgroups
   // run concurrently and the repeat weight reads of the later chunks hit the caches)
@@ -385,7 +387,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
   } else {
     p.M = min(p0.zrows, p0.M);
   }
-  dec_linear_body<KTM, NCB, LNA, EPI, TC, false>(p, ksn, blockIdx.x, blockIdx.y, blockDim.x >> 6, MlpPub{});
+  dec_linear_body<KTM, NCB, LNA, EPI, TC, false, H2>(p, ksn, blockIdx.x, blockIdx.y, blockDim.x >> 6, MlpPub{});
 }
 
 // ---- fused decode MLP: fc1 (LayerNorm-fused, GELU) -> fc2 (+ residual) in ONE launch (kw_dec_mlp) ----
@@ -1108,6 +1110,10 @@ Geo choose(int64_t N, int64_t K) {
 // 1,621-workgroup grid keeps direct fragment loads at four workgroups per CU.
 bool use_xlds(int64_t N, const Geo& g) { return g.ks > 1 || (N + 16 * g.ncb - 1) / (16 * g.ncb) <= 256; }
 size_t x_lds_bytes_for(int nkt, int ks, bool xlds) { return xlds ? x_lds_bytes((nkt + ks - 1) / ks) : 0; }
+// the image of a <= 16-row chunk (row split): only its rows' pieces are staged
+size_t x_lds_bytes_rows(int tiles, int rows, bool xlds) {
+  return xlds ? (size_t)((rows * (4 * tiles + 1) + 63) / 64) * 1024 : 0;
+}
 
 bool row_split_on() {
 #ifdef KW_LAB_OVERRIDES
@@ -1132,6 +1138,19 @@ int device_cus() {
   return ncu;
 }
 
+template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool H2>
+hipError_t launch_grid(const DecP& q, dim3 grid, dim3 block, size_t shm, int ks, hipStream_t s) {
+  static size_t attr = 0;  // dynamic LDS this instantiation is cleared for
+  if (shm > attr) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dec_linear_kernel<KTM, NCB, LNA, EPI, TC, H2>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
+    if (e != hipSuccess) return e;
+    attr = shm;
+  }
+  hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, EPI, TC, H2>), grid, block, shm, s, q, ks);
+  return hipGetLastError();
+}
+
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
 hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
   const int nkt = p.K / 32;
@@ -1143,24 +1162,18 @@ hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
                        dim3((unsigned)(64 * g.nw)), 0, s, p, zper);
     return hipGetLastError();
   }
-  const size_t shm = x_lds_bytes_for(nkt, g.ks, p.xlds);
-  static size_t attr = 0;  // dynamic LDS this instantiation is cleared for
-  if (shm > attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dec_linear_kernel<KTM, NCB, LNA, EPI, TC>),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    if (e != hipSuccess) return e;
-    attr = shm;
-  }
-  // row split: a grid of at most 128 column groups (the 1280-column linears: 80 workgroups on 256 CUs) runs its
-  // 17..32 rows as two 16-row chunks -- twice the workgroups, each staging half the activation rows (every output
-  // element is computed by the same operations: rows are independent)
-  DecP q = p;
+  // row split: a grid of at most one workgroup per CU (the 1280-column linears: 80 workgroups; fc1: 160) runs its
+  // 17..32 rows as two 16-row chunks -- twice the workgroups, each staging only its rows and computing one row half
+  // (the H2 = false instantiation: its registers and LDS allow two workgroups per CU), every output element by the
+  // same operations (rows are independent): bitwise the 32-row launch
   const int ncg = (p.N + 16 * NCB - 1) / (16 * NCB);
-  q.zrows = (g.ks == 1 && p.M > 16 && p.M <= 32 && ncg <= 128 && row_split_on()) ? 16 : 32;
+  const bool split = g.ks == 1 && p.M > 16 && p.M <= 32 && ncg <= device_cus() && row_split_on();
+  DecP q = p;
+  q.zrows = split ? 16 : 32;
   const dim3 grid((unsigned)ncg, (unsigned)g.ks, (unsigned)((p.M + q.zrows - 1) / q.zrows));
   const dim3 block((unsigned)(64 * g.nw));
-  hipLaunchKernelGGL((dec_linear_kernel<KTM, NCB, LNA, EPI, TC>), grid, block, shm, s, q, g.ks);
-  return hipGetLastError();
+  if (split) return launch_grid<KTM, NCB, LNA, EPI, TC, false>(q, grid, block, x_lds_bytes_rows((nkt + g.ks - 1) / g.ks, 16, p.xlds), g.ks, s);
+  return launch_grid<KTM, NCB, LNA, EPI, TC, true>(q, grid, block, x_lds_bytes_for(nkt, g.ks, p.xlds), g.ks, s);
 }
 
 template <int KTM, int NCB>
