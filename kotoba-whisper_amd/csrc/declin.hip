@@ -1162,12 +1162,13 @@ hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
                        dim3((unsigned)(64 * g.nw)), 0, s, p, zper);
     return hipGetLastError();
   }
-  // row split: a grid of at most one workgroup per CU (the 1280-column linears: 80 workgroups; fc1: 160) runs its
-  // 17..32 rows as two 16-row chunks -- twice the workgroups, each staging only its rows and computing one row half
-  // (the H2 = false instantiation: its registers and LDS allow two workgroups per CU), every output element by the
-  // same operations (rows are independent): bitwise the 32-row launch
+  // row split: a grid whose doubled size still fits one round of one workgroup per CU (the 1280-column linears: 80
+  // workgroups -> 160) runs its 17..32 rows as two 16-row chunks, each staging only its rows and computing one row
+  // half (the H2 = false instantiation), every output element by the same operations (rows are independent):
+  // bitwise the 32-row launch.  o 5.05 -> 4.13-4.29 us; fc1 (160 -> 320 workgroups, two per CU) measured
+  // 8.6 -> 8.7-8.9 us, so it keeps one launch of 32-row tiles (profiles/r04o_rowsplit_ab.txt)
   const int ncg = (p.N + 16 * NCB - 1) / (16 * NCB);
-  const bool split = g.ks == 1 && p.M > 16 && p.M <= 32 && ncg <= device_cus() && row_split_on();
+  const bool split = g.ks == 1 && p.M > 16 && p.M <= 32 && 2 * ncg <= device_cus() && row_split_on();
   DecP q = p;
   q.zrows = split ? 16 : 32;
   const dim3 grid((unsigned)ncg, (unsigned)g.ks, (unsigned)((p.M + q.zrows - 1) / q.zrows));
