@@ -1115,17 +1115,15 @@ size_t x_lds_bytes_rows(int tiles, int rows, bool xlds) {
   return xlds ? (size_t)((rows * (4 * tiles + 1) + 63) / 64) * 1024 : 0;
 }
 
-// 1: row split for single-round K-unsplit grids (the product); lab builds: KW_DECLIN_ROWSPLIT=0 off, =2 also the
-// K-split grids (fc2), for A/B
-int row_split_mode() {
+bool row_split_on() {
 #ifdef KW_LAB_OVERRIDES
-  static const int mode = [] {
+  static const bool on = [] {  // lab builds: KW_DECLIN_ROWSPLIT=0 turns the row split off (A/B)
     const char* e = getenv("KW_DECLIN_ROWSPLIT");
-    return e ? atoi(e) : 1;
+    return !(e && e[0] == '0');
   }();
-  return mode;
+  return on;
 #else
-  return 1;
+  return true;
 #endif
 }
 
@@ -1170,8 +1168,7 @@ hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
   // bitwise the 32-row launch.  o 5.05 -> 4.13-4.29 us; fc1 (160 -> 320 workgroups, two per CU) measured
   // 8.6 -> 8.7-8.9 us, so it keeps one launch of 32-row tiles (profiles/r04o_rowsplit_ab.txt)
   const int ncg = (p.N + 16 * NCB - 1) / (16 * NCB);
-  const int rsm = row_split_mode();
-  const bool split = p.M > 16 && p.M <= 32 && 2 * ncg <= device_cus() && (g.ks == 1 ? rsm >= 1 : rsm >= 2);
+  const bool split = g.ks == 1 && p.M > 16 && p.M <= 32 && 2 * ncg <= device_cus() && row_split_on();
   DecP q = p;
   q.zrows = split ? 16 : 32;
   const dim3 grid((unsigned)ncg, (unsigned)g.ks, (unsigned)((p.M + q.zrows - 1) / q.zrows));

@@ -2,6 +2,7 @@
 # r04: fc2 (N 1280 x K 5120, K-split) with and without the row split (KW_DECLIN_ROWSPLIT=2 lets the K-split grids
 # run two 16-row chunks too) over K-split geometries (KW_DECLIN_GEO="N,K,ncb,ktm,ks"; lab build, ctypes backend).
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
+# lab library: bash tools/lab/mlp_lab_build.sh tools/lab/fc2_rowsplit.diff
 export KWHISPER_LIB="$PWD/kotoba-whisper_amd/kwhisper/libkwhisper_lab.so"
 for rep in 1 2; do
   for cfg in default 1280,5120,1,10,3 1280,5120,1,10,4 1280,5120,1,5,4 1280,5120,1,5,8; do
