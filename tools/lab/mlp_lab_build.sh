@@ -11,7 +11,7 @@ mkdir -p "$T/kotoba-whisper_amd" "$T/include"
 cp -r "$ROOT/kotoba-whisper_amd/csrc" "$T/kotoba-whisper_amd/csrc"
 rm -rf "$T/kotoba-whisper_amd/csrc/build" "$T/kotoba-whisper_amd/csrc/build_lab"
 cp "$ROOT/include/kwhisper.h" "$T/include/"
-PATCH="${1:-$ROOT/tools/lab/mlp_lab.diff}"
+PATCH="$(realpath "${1:-$ROOT/tools/lab/mlp_lab.diff}")"
 (cd "$T" && patch -p1 < "$PATCH")
 make -C "$T/kotoba-whisper_amd/csrc" -j8 EXTRA=-DKW_LAB_OVERRIDES BUILD=build_lab \
   OUT="$ROOT/kotoba-whisper_amd/kwhisper/libkwhisper_lab.so" TORCH_OUT="$ROOT/kotoba-whisper_amd/kwhisper/libkwhisper_torch_lab.so"
