@@ -596,17 +596,18 @@ def test_config4_bf16_pseudo_label_w1_w2(c4_gold, tmp_path):
     print("config4 bf16 pseudo_label: W=2 (gloo, 2 processes on cuda:0, batch 16 each) == W=1 on 32 items")
 
 
-def test_large_v3_longform_multipass(gold):
+@pytest.mark.parametrize("fixture", ["large_v3_longform_fp32", "large_v3_longform8_fp32"])
+def test_large_v3_longform_multipass(gold, fixture):
     """The seek loop's second and later passes at large-v3.  No config-4 stand-in clip takes a
     second pass under transformers' fp32 large-v3 at max_length 128 (all 1,768 scanned on the oracle log-mel,
     profiles/r04d_multipass_scan.json), so the multi-pass path -- the re-encode of the mel shifted to the last
     timestamp, the cumulative max_length growth (generation_whisper.py:785-903,1935-1940), the batch shrinking as
-    rows finish -- is pinned on two > 30 s clips batched with the frame mask at the config-4 settings
-    (tests/golden/large_v3_longform_fp32.npz): the fp32 engine bit-exact with per-row pass counts equal to
-    transformers' (>= 2 each), the bf16 engine margin-gated."""
+    rows finish -- is pinned on > 30 s clips batched with the frame mask at the config-4 settings
+    (tests/golden/large_v3_longform_fp32.npz: 2 clips; large_v3_longform8_fp32.npz: 8 clips of 33-88 s): the fp32
+    engine bit-exact with per-row pass counts equal to transformers' (>= 2 each), the bf16 engine margin-gated."""
     from _util import longform_inputs
 
-    g = gold("large_v3_longform_fp32")
+    g = gold(fixture)
     feats, mask, _ = longform_inputs(g["clips"], n_mels=LARGE_V3.num_mel_bins)
     feats, mask = torch.from_numpy(feats).cuda(), torch.from_numpy(mask).cuda()
     kw = dict(language="ja", task="transcribe", return_timestamps=True, max_length=int(g["max_length"]))
@@ -621,7 +622,7 @@ def test_large_v3_longform_multipass(gold):
     t16 = m16.generate(feats, attention_mask=mask, **kw).cpu().numpy()
     w = min(t16.shape[1], g["tokens"].shape[1])
     n = _gated_equal(t16[:, :w], g["tokens"][:, :w], g["margin"][:, :w])
-    print(f"\nlarge-v3 long-form: passes per row {g['passes'].tolist()} (fp32 engine bit-exact, same passes); bf16 "
+    print(f"\n{fixture}: passes per row {g['passes'].tolist()} (fp32 engine bit-exact, same passes); bf16 "
           f"{n} of {g['tokens'].size} tokens compared (margin >= {MARGIN_FLOOR}), all equal; bf16 passes "
           f"{m16.stats['row_passes'].tolist()}")
     del m16

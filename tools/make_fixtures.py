@@ -393,9 +393,12 @@ def large_config4_multipass_fixtures(ids_json):
 
 
 LARGE_LONG_CLIPS = [("tone", 0, 45.0), ("dummy", 3, 70.0)]
+# r04: eight more > 30 s clips (33-88 s) in one batch -- the multi-pass path on >= 8 rows
+LARGE_LONG8_CLIPS = [("tone", 1, 38.0), ("dummy", 4, 52.0), ("tone", 2, 61.0), ("dummy", 5, 33.0),
+                     ("tone", 3, 88.0), ("dummy", 6, 44.0), ("tone", 4, 57.0), ("dummy", 7, 75.0)]
 
 
-def large_longform_fixtures():
+def large_longform_fixtures(name="large_v3_longform_fp32", clips=None):
     """tests/golden/large_v3_longform_fp32.npz: the seek loop's SECOND and later passes at large-v3 (VERDICT r3 item
     1).  No config-4 stand-in clip takes a second pass in transformers' fp32 large-v3 at max_length 128 (every one of
     the 1,768 clips is single-pass: profiles/r04d_multipass_scan.json), so the multi-pass path -- re-encoding the mel
@@ -406,7 +409,8 @@ def large_longform_fixtures():
     t0 = time.time()
     m = hf_model(LARGE_V3)
     fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins)
-    audio = [long_audio(k, s, sec) for k, s, sec in LARGE_LONG_CLIPS]
+    clips = LARGE_LONG_CLIPS if clips is None else clips
+    audio = [long_audio(k, s, sec) for k, s, sec in clips]
     inp = fe(audio, sampling_rate=16000, return_tensors="pt", truncation=False, padding="longest",
              return_attention_mask=True)
     m.generation_config, gc = hf_gen_config(LARGE_V3)
@@ -423,10 +427,10 @@ def large_longform_fixtures():
         assert np.array_equal(tk, toks[b, : len(tk)]) and (toks[b, len(tk):] == gc.pad_token_id).all()
         margin[b, : len(mg)] = mg
     segs = [[(float(x["start"]), float(x["end"]), len(x["tokens"])) for x in row] for row in res["segments"]]
-    out = {"clips": np.array([f"{k}:{s}:{sec}" for k, s, sec in LARGE_LONG_CLIPS]), "tokens": toks, "margin": margin,
+    out = {"clips": np.array([f"{k}:{s}:{sec}" for k, s, sec in clips]), "tokens": toks, "margin": margin,
            "passes": passes, "segments": np.array(json.dumps(segs)), "max_length": 128}
-    np.savez_compressed(os.path.join(GOLD, "large_v3_longform_fp32.npz"), **out)
-    print(f"large_v3_longform fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
+    np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), **out)
+    print(f"{name} fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
 
 
 KOTOBA_BEAM_CASES = [("tone", 0), ("dummy", 0), ("tone", 2), ("dummy", 3)]
@@ -601,6 +605,8 @@ def main():
         large_config4_fixtures()
     if not a.skip_large and a.only == "large_longform":
         large_longform_fixtures()
+    if not a.skip_large and a.only == "large_longform8":
+        large_longform_fixtures("large_v3_longform8_fp32", LARGE_LONG8_CLIPS)
     if not a.skip_large and a.only == "large_c4_mp":
         large_config4_multipass_fixtures(a.multipass_ids)
     if not a.skip_large and a.only in (None, "kotoba_beam"):
