@@ -434,3 +434,26 @@ def test_lanes_return_the_single_lane_predictions(n, bs, lanes):
         assert list(steps[si]) in [list(b) for b in h.batches]
     with pytest.raises(ValueError, match="gather"):
         pseudo_label(_LaneStub(), _features, 3, batch_size=4, pad_token_id=PAD, lanes=2)
+
+
+def test_lanes_checkpoint_resume(tmp_path):
+    """lanes=2 with checkpoint_dir: the lane threads write each step's per-rank file; a rerun (any lane count)
+    decodes nothing and returns the same predictions; a partial directory resumes only the missing steps."""
+    ck = tmp_path / "ck"
+    ref = pseudo_label(_StubModel(), _features, 23, batch_size=4, pad_token_id=PAD, gather="end")
+    m = _LaneStub()
+    got = pseudo_label(m, _features, 23, batch_size=4, pad_token_id=PAD, gather="end", lanes=2, checkpoint_dir=str(ck))
+    _same(got, ref)
+    m2 = _LaneStub()
+    again = pseudo_label(m2, _features, 23, batch_size=4, pad_token_id=PAD, gather="end", lanes=3,
+                         checkpoint_dir=str(ck))
+    _same(again, ref)
+    assert sum(len(h.batches) for h in m2.lanes) == 0
+    victims = sorted(ck.glob("round_*_rank0.npz"))[1::2]
+    for v in victims:
+        v.unlink()
+    m3 = _LaneStub()
+    part = pseudo_label(m3, _features, 23, batch_size=4, pad_token_id=PAD, gather="end", lanes=2,
+                        checkpoint_dir=str(ck))
+    _same(part, ref)
+    assert sum(len(h.batches) for h in m3.lanes) == len(victims)
