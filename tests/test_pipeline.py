@@ -315,3 +315,48 @@ def test_pipeline_lanes_match_one_lane(lanes):
     assert sum(h.calls for h in m.handles) == 2 * m1.calls
     with pytest.raises(ValueError, match="lane"):
         ASRPipeline(_StubASRModel(), feature_extractor=_StubFE(), lanes=2)
+
+
+def _dp_lanes_worker(rank, world, port, out_dir):
+    import json
+
+    import torch.distributed as dist
+
+    from kwhisper.pipeline import ASRPipeline
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        m = _LaneASRModel()
+        got = ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=1, lanes=2)(_dp_clips())
+        with open(os.path.join(out_dir, f"l{rank}.json"), "w") as f:
+            json.dump({"res": got, "calls": sum(h.calls for h in m.handles)}, f,
+                      default=lambda x: x.tolist() if hasattr(x, "tolist") else x)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipeline_data_parallel_with_lanes_gloo():
+    """Both at once: window batches round-robin over two gloo ranks, each rank decoding its share on two lanes;
+    every rank's merged output equals the single-process, single-lane run's."""
+    import json
+    import socket
+    import tempfile
+
+    import torch.multiprocessing as mp
+
+    from kwhisper.pipeline import ASRPipeline
+
+    m1 = _StubASRModel()
+    want = json.loads(json.dumps(ASRPipeline(m1, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=1)(_dp_clips()),
+                                 default=lambda x: x.tolist() if hasattr(x, "tolist") else x))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_dp_lanes_worker, args=(2, port, d), nprocs=2, join=True)
+        calls = 0
+        for r in range(2):
+            z = json.load(open(os.path.join(d, f"l{r}.json")))
+            assert z["res"] == want
+            calls += z["calls"]
+    assert calls == m1.calls
