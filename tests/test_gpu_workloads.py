@@ -721,3 +721,26 @@ def test_config4_pseudo_label_resume_engine(tiny32, tmp_path):
     assert ids2 == ids1 == list(range(N_ITEMS))
     for a, b in zip(preds1, preds2):
         np.testing.assert_array_equal(a, b)
+
+
+def test_pseudo_label_lanes_engine(tiny32):
+    """pseudo_label(gather="end", lanes=2 / 3) over the HIP engine: batches decode concurrently on model.lane()
+    handles from host threads, each on its own stream (graph capture thread-local, stream-local syncs); the
+    predictions equal the one-lane run's, and step_model() names the handle that decoded each step."""
+    from kwhisper.pseudo_label import pseudo_label, step_model
+
+    pad = tiny32.generation_config.eos_token_id
+    ids1, preds1 = pseudo_label(tiny32, _item_features, N_ITEMS, batch_size=BS, gen_kwargs=GEN_KW, pad_token_id=pad,
+                                gather="end")
+    for lanes in (2, 3):
+        handles = {}
+
+        def on_step(si, total):
+            handles[si] = step_model()
+
+        ids2, preds2 = pseudo_label(tiny32, _item_features, N_ITEMS, batch_size=BS, gen_kwargs=GEN_KW,
+                                    pad_token_id=pad, gather="end", lanes=lanes, on_step=on_step)
+        assert ids2 == ids1
+        for a, b in zip(preds1, preds2):
+            np.testing.assert_array_equal(a, b)
+        assert len({id(h) for h in handles.values()}) == min(lanes, len(handles))
