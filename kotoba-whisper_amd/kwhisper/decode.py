@@ -11,9 +11,14 @@ LM head with the final LayerNorm fused + sampler) is captured once into a hipGra
 reads its position from device memory, so one graph serves every step.  The host only polls the
 device unfinished-row count a few steps behind the GPU (no per-step sync).  Graphs are captured with
 capture_error_mode="thread_local", so another host thread (another batch in flight on its own stream,
-WhisperEngine.lane()) may keep launching while one session captures.
+WhisperEngine.lane()) may keep launching while one session captures.  Captures themselves are serialised by one
+process-wide lock (``CAPTURE_LOCK``): ``torch.cuda.graph.__enter__`` synchronises the whole device and empties the
+allocator cache, which must not run inside another thread's capture; session creation (allocations) takes the same
+lock.
 """
 from __future__ import annotations
+
+import threading
 
 import numpy as np
 import torch
@@ -23,6 +28,20 @@ from . import ops
 
 _HD = 64
 T_MAX = 448
+# serialises every hipGraph capture and every session allocation of the process (lanes capture on host threads)
+CAPTURE_LOCK = threading.RLock()
+
+
+def capture_graph(fn, dev) -> torch.cuda.CUDAGraph:
+    """Capture ``fn``'s launches into a new graph on a side stream, under CAPTURE_LOCK."""
+    with CAPTURE_LOCK:
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+            fn()
+        torch.cuda.current_stream(dev).wait_stream(side)
+    return g
 
 
 class DecodeSession:
@@ -402,13 +421,7 @@ class DecodeSession:
 
         pg = cfg.get("prefill_graph")
         if pg is None and use_graph and not record_scores:
-            pg = torch.cuda.CUDAGraph()
-            side = torch.cuda.Stream(device=dev)
-            side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.graph(pg, stream=side, capture_error_mode="thread_local"):
-                prefill()
-            torch.cuda.current_stream(dev).wait_stream(side)
-            cfg["prefill_graph"] = pg
+            pg = cfg["prefill_graph"] = capture_graph(prefill, dev)
             # capture only records: the kernels have not run yet, and the state the prefill consumes
             # (ids, cur_len, counters) is untouched -- replay below
         if pg is not None and use_graph and not record_scores:
@@ -428,14 +441,10 @@ class DecodeSession:
             sampler()
 
         def capture(n):
-            g = torch.cuda.CUDAGraph()
-            side = torch.cuda.Stream(device=dev)
-            side.wait_stream(torch.cuda.current_stream(dev))
-            with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
+            def steps():
                 for _ in range(n):
                     one_step()
-            torch.cuda.current_stream(dev).wait_stream(side)
-            return g
+            return capture_graph(steps, dev)
 
         graph = cfg["graph"]
         if graph is None and use_graph and not record_scores and n_steps > 1:
@@ -561,13 +570,7 @@ class DecodeSession:
         def captured(name, fn):
             g = cfg[name]
             if g is None:
-                g = torch.cuda.CUDAGraph()
-                side = torch.cuda.Stream(device=dev)
-                side.wait_stream(torch.cuda.current_stream(dev))
-                with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
-                    fn()
-                torch.cuda.current_stream(dev).wait_stream(side)
-                cfg[name] = g
+                g = cfg[name] = capture_graph(fn, dev)
             return g
 
         if use_graph:

@@ -344,6 +344,7 @@ class WhisperEngine:
         return other
 
     def new_session(self, B: int, enc: torch.Tensor | None = None, beams: int = 1) -> "DecodeSession":
-        from .decode import DecodeSession
+        from .decode import CAPTURE_LOCK, DecodeSession
 
-        return DecodeSession(self, B, enc, beams=beams)
+        with CAPTURE_LOCK:  # allocations must not interleave with another lane's capture
+            return DecodeSession(self, B, enc, beams=beams)

@@ -211,6 +211,29 @@ def _dist():
     return dist if dist.is_available() and dist.is_initialized() else None
 
 
+def _check_same_inputs(dist, flat) -> None:
+    """data_parallel splits the window batches over the ranks on the assumption that every rank holds the same
+    windows: all-reduce (MAX of x and of -x) of the window count and of a digest of every window's item index,
+    sample count and first / last samples; raise on any difference (a per-rank shard of files would otherwise give
+    position j the tokens of another rank's audio, or hang the gather on mismatched shapes)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for i, c in flat:
+        a = np.asarray(c["audio"].cpu() if torch.is_tensor(c["audio"]) else c["audio"], dtype=np.float32).reshape(-1)
+        h.update(np.array([i, a.size], dtype=np.int64).tobytes())
+        h.update(a[:16].tobytes() + a[-16:].tobytes())
+    sig = [len(flat), int.from_bytes(h.digest()[:6], "little")]
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor(sig + [-x for x in sig], dtype=torch.int64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    hi, lo = t[:2].cpu().tolist(), [-x for x in t[2:].cpu().tolist()]
+    if hi != lo:
+        raise ValueError("ASRPipeline(data_parallel=True) needs the same inputs on every rank (window counts "
+                         f"{lo[0]}..{hi[0]}, or the audio differs); shard the inputs yourself and use "
+                         "data_parallel=False instead")
+
+
 class ASRPipeline:
     """``pipeline("automatic-speech-recognition", model=<whisper>, chunk_length_s=..., batch_size=...)`` for
     the MI355X engine (TF/pipelines/automatic_speech_recognition.py, seq2seq_whisper path).
@@ -220,7 +243,7 @@ class ASRPipeline:
 
     def __init__(self, model, feature_extractor=None, tokenizer=None, *, chunk_length_s: float = 0,
                  stride_length_s=None, batch_size: int = 1, generate_kwargs: Optional[dict] = None,
-                 return_timestamps=None, data_parallel: bool = True, lanes: int = 1):
+                 return_timestamps=None, data_parallel: bool = False, lanes: int = 1):
         from .feature_extraction import WhisperFeatureExtractor
 
         self.model = model
@@ -232,8 +255,10 @@ class ASRPipeline:
         self.batch_size = max(1, int(batch_size))
         self.generate_kwargs = dict(generate_kwargs or {})
         self.return_timestamps = return_timestamps
-        # with a torch.distributed process group: window batches round-robin over the ranks, one gather of the
-        # token matrices at the end, every rank returns the full result (config 5 at W GPUs)
+        # data_parallel (opt-in) with a torch.distributed process group: every rank passes the SAME inputs, window
+        # batches go round-robin over the ranks, one gather of the token matrices at the end, every rank returns the
+        # full result (config 5 at W GPUs).  The ranks' inputs are checked to agree before the split
+        # (_check_same_inputs); transformers' pipeline itself has no cross-rank behaviour, hence off by default
         self.data_parallel = bool(data_parallel)
         # lanes > 1: that many window batches decode at once on model.lane() handles (shared weights), one host
         # thread and stream each -- one batch's latency-bound decode chain beside another's HBM-bound
@@ -441,6 +466,8 @@ class ASRPipeline:
         tokens = [None] * len(flat)
         starts = list(range(0, len(flat), bs))
         dist = _dist() if self.data_parallel else None
+        if dist is not None:
+            _check_same_inputs(dist, flat)
         world, rank = (dist.get_world_size(), dist.get_rank()) if dist is not None else (1, 0)
         mine = starts[rank::world]  # data parallel: window batch j on rank j % W, no collective until the end
         local = self._decode_batches([flat[b0: b0 + bs] for b0 in mine], gk)

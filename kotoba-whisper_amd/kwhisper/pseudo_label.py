@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 __all__ = ["shard_batches", "gather_remainder", "pad_across_processes", "gather_matrices", "pseudo_label",
-           "pseudo_label_multitask",
+           "pseudo_label_multitask", "last_schedule",
            "legacy_prompt", "write_transcription_csv", "transcription_table", "write_transcription_arrow"]
 
 
@@ -139,6 +139,10 @@ def _rank_round_path(checkpoint_dir: str, si: int, rank: int) -> str:
     return os.path.join(checkpoint_dir, f"round_{si:06d}_rank{rank:03d}.npz")
 
 
+def _batch_path(checkpoint_dir: str, j: int) -> str:
+    return os.path.join(checkpoint_dir, f"batch_{j:06d}.npz")
+
+
 def weights_fingerprint(model) -> Optional[str]:
     """A short digest of a few of the model's weight values (the token embedding's first rows and the decoder's
     last layer's fc2 bias), so a resume with other weights of the same architecture is refused; None for a
@@ -172,12 +176,14 @@ def run_digest(model, **config) -> str:
     return hashlib.sha256(blob.encode()).hexdigest()
 
 
-def _plan_matches(stored: dict, plan: dict) -> bool:
-    """plan.json equality; a plan written before the configuration digest existed (no ``config_sha256``) is
-    accepted as legacy with a warning when everything else matches."""
+def _plan_matches(stored: dict, plan: dict, allow_legacy: bool = False) -> bool:
+    """plan.json equality.  A plan written before the configuration digest existed (no ``config_sha256``) cannot
+    prove that its rounds were decoded with this run's generate kwargs and weights, so it is refused unless the
+    caller opts in (``allow_legacy_checkpoint=True``), and then resumed with a warning."""
     if stored == plan:
         return True
-    if "config_sha256" not in stored and {k: v for k, v in plan.items() if k != "config_sha256"} == stored:
+    legacy = "config_sha256" not in stored and {k: v for k, v in plan.items() if k != "config_sha256"} == stored
+    if legacy and allow_legacy:
         import warnings
 
         warnings.warn("checkpoint plan.json predates the configuration digest: resuming without checking that the "
@@ -186,12 +192,14 @@ def _plan_matches(stored: dict, plan: dict) -> bool:
     return False
 
 
-def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict, rank_files: int = 0) -> List[bool]:
+def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict, rank_files: int = 0,
+                 batch_files: bool = False, allow_legacy: bool = False) -> List[bool]:
     """Which gathered rounds already have a checkpoint file, as rank 0 sees it (broadcast: every rank skips
     the same rounds, so the per-round collectives stay matched).  The directory's ``plan.json`` (items,
     batch size, world size, and the digest of the generate kwargs / output layout / model) must match this
     run's: the rounds of another plan hold other items or other labels.  ``rank_files`` = W (deferred gather):
-    a round counts as done when every rank's own file of it exists."""
+    a round counts as done when every rank's own file of it exists.  ``batch_files`` (dynamic schedule): entry j is
+    global batch j's ``batch_<j>.npz``."""
     if not checkpoint_dir or n_steps == 0:
         return [False] * n_steps
     import json
@@ -203,14 +211,16 @@ def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict
         meta = os.path.join(checkpoint_dir, "plan.json")
         if os.path.exists(meta):
             with open(meta) as f:
-                mask[0] = int(not _plan_matches(json.load(f), plan))
+                mask[0] = int(not _plan_matches(json.load(f), plan, allow_legacy))
         else:
             with open(meta + ".tmp", "w") as f:
                 json.dump(plan, f)
             os.replace(meta + ".tmp", meta)
         if not int(mask[0]):
             for si in range(n_steps):
-                if rank_files:
+                if batch_files:
+                    ok = os.path.exists(_batch_path(checkpoint_dir, si))
+                elif rank_files:
                     ok = all(os.path.exists(_rank_round_path(checkpoint_dir, si, r)) for r in range(rank_files))
                 else:
                     ok = os.path.exists(_round_path(checkpoint_dir, si))
@@ -219,29 +229,34 @@ def _done_rounds(checkpoint_dir: Optional[str], n_steps: int, device, plan: dict
         dist.broadcast(mask, 0)
     m = mask.cpu().tolist()
     if m[0]:
-        raise ValueError(f"checkpoint_dir {checkpoint_dir} holds rounds of another plan than {plan} (plan.json)")
+        raise ValueError(f"checkpoint_dir {checkpoint_dir} holds rounds of another plan than {plan} (plan.json; a plan "
+                         "without config_sha256 predates the digest: pass allow_legacy_checkpoint=True to resume it)")
     return [bool(x) for x in m[1:]]
 
 
-def _save_round(checkpoint_dir: str, si: int, fid: List[int], mats: List[np.ndarray], path: Optional[str] = None) -> None:
+def _save_round(checkpoint_dir: str, si: int, fid: List[int], mats: List[np.ndarray], path: Optional[str] = None,
+                rank: Optional[int] = None) -> None:
     path = path or _round_path(checkpoint_dir, si)
-    tmp = f"{path}.{os.getpid()}.tmp"
+    tmp = f"{path}.{os.getpid()}.{threading.get_ident()}.tmp"
+    extra = {} if rank is None else {"rank": np.asarray(rank, dtype=np.int64)}  # dynamic schedule: who decoded it
     with open(tmp, "wb") as f:
-        np.savez(f, fid=np.asarray(fid, dtype=np.int64), **{f"c{c}": m for c, m in enumerate(mats)})
+        np.savez(f, fid=np.asarray(fid, dtype=np.int64), **extra, **{f"c{c}": m for c, m in enumerate(mats)})
     os.replace(tmp, path)  # atomic: a restart sees the whole round or none of it
 
 
 def _load_round(checkpoint_dir: str, si: int, path: Optional[str] = None):
     with np.load(path or _round_path(checkpoint_dir, si), allow_pickle=False) as z:
-        n_cols = sum(1 for k in z.files if k.startswith("c"))
+        n_cols = sum(1 for k in z.files if k.startswith("c") and k[1:].isdigit())
         return z["fid"].tolist(), [z[f"c{c}"] for c in range(n_cols)]
 
 
 def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                checkpoint_dir=None, digest=None):
+                checkpoint_dir=None, digest=None, schedule="static", allow_legacy=False):
     """Shared DP loop: ``decode(feats)`` -> list of id matrices (one per output column); each is padded
     across ranks and gathered with the file ids (``run_pseudo_labelling.py:336-344``, v3 ``:309-321``).
     With ``checkpoint_dir``, gathered rounds are checkpointed and rounds already on disk are skipped."""
+    if schedule != "static":
+        raise ValueError("schedule='dynamic' needs gather='end' (the per-round gather keeps the ranks in lock step)")
     dist = _dist()
     world = dist.get_world_size() if dist else 1
     rank = dist.get_rank() if dist else 0
@@ -254,7 +269,7 @@ def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device,
         else torch.device("cpu"))
     done = _done_rounds(checkpoint_dir, len(steps), mask_dev,
                         {"n_items": int(n_items), "batch_size": int(batch_size), "world_size": int(world),
-                         "config_sha256": digest})
+                         "config_sha256": digest}, allow_legacy=allow_legacy)
     eval_ids: List[int] = []
     cols: Optional[List[List[np.ndarray]]] = None
     for si, idx in enumerate(steps):
@@ -299,36 +314,100 @@ def _label_loop(model, features, n_items, batch_size, pad_token_id, comm_device,
     return eval_ids, cols or []
 
 
+class _Claims:
+    """The next global batch index for a worker (a rank's lane thread): ONE counter shared by every rank, held in the
+    process group's own key-value store (``Store.add`` on the rendezvous TCPStore: a host round trip, the GPU is never
+    involved), so the next batch goes to the first idle worker anywhere in the job.  Without a process group: a local
+    counter.  ``order`` maps the k-th claim to a global batch index (the batches not already on disk)."""
+
+    _calls = 0  # per process; every rank makes the same sequence of pseudo_label calls, so keys match
+
+    def __init__(self, dist, order: List[int]):
+        self.order, self.lock = order, threading.Lock()
+        self.store, self.key, self.local = None, None, 0
+        if dist is not None:
+            from torch.distributed import distributed_c10d as c10d
+
+            _Claims._calls += 1
+            self.store = c10d._get_default_store()
+            self.key = f"kwhisper/pseudo_label/{_Claims._calls}/next"
+
+    def next(self) -> Optional[int]:
+        with self.lock:  # one store client per process: lane threads take turns
+            if self.store is not None:
+                k = int(self.store.add(self.key, 1)) - 1
+            else:
+                k, self.local = self.local, self.local + 1
+        return self.order[k] if k < len(self.order) else None
+
+
+_LAST_SCHEDULE: List[int] = []
+
+
+def last_schedule() -> List[int]:
+    """After a ``schedule="dynamic"`` call: the rank that decoded each global batch (round si, rank slot r ->
+    index si * W + r of the reference's plan), -1 for a batch read back from ``checkpoint_dir``."""
+    return list(_LAST_SCHEDULE)
+
+
 def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                         checkpoint_dir=None, digest=None):
+                         checkpoint_dir=None, digest=None, schedule="static", allow_legacy=False):
     """``_label_loop`` with the per-round collectives deferred to ONE exchange at the end (``gather="end"``).
 
     The reference pads and gathers after every batch (run_pseudo_labelling.py:339-341), so every round waits
     for the slowest rank's batch; with timestamps a batch's cost depends on its seek passes, so that lock step
-    loses throughput at W > 1.  Here each rank decodes its whole shard (accelerate's plan, ``shard_batches``)
-    without a collective, keeps its per-batch matrices and widths, and at the end one all-reduce(MAX) of the
-    width and two all-gathers (per-round widths, the padded token rows) rebuild exactly the rounds the
-    per-batch gather would have produced: each round's rows padded to that round's widest rank, the wrapped
-    duplicates of the final round dropped, file ids from the (deterministic) shard plan of every rank.
-    Resume: each rank checkpoints its own batches (``round_<step>_rank<r>.npz``); a round counts as done when
-    every rank's file of it exists (rank 0's view, broadcast once)."""
+    loses throughput at W > 1.  Here each rank decodes its batches without a collective, keeps its per-batch
+    matrices and widths, and at the end one all-reduce(MAX) of the width and two all-gathers (per-batch shapes, the
+    padded token rows) rebuild exactly the rounds the per-batch gather would have produced: each round's rows padded
+    to that round's widest rank, the wrapped duplicates of the final round dropped, file ids from the
+    (deterministic) shard plan of every rank.
+
+    ``schedule="static"``: rank r decodes accelerate's batches r, r + W, ... (``shard_batches``).  Resume: each rank
+    checkpoints its own batches (``round_<step>_rank<r>.npz``); a round counts as done when every rank's file of it
+    exists (rank 0's view, broadcast once).
+    ``schedule="dynamic"``: the same W x n_steps batches (identical item sets, so identical outputs -- the decode of a
+    batch does not depend on the process that runs it), but each worker (every lane of every rank) takes the NEXT
+    undecoded batch when it becomes idle (``_Claims``: list scheduling), so a rank that drew a slow batch (several seek
+    passes) no longer holds the others back.  Resume: one file per global batch (``batch_<j>.npz``, with the rank that
+    decoded it); batches on disk are skipped and read back by every rank.  ``last_schedule()`` reports who decoded what.
+    ``on_step(step, total)`` is called from the decoding thread, one call at a time (a lock), in completion order;
+    ``step`` is the rank's step index (static) or the global batch index (dynamic)."""
+    global _LAST_SCHEDULE
     dist = _dist()
     world = dist.get_world_size() if dist else 1
     rank = dist.get_rank() if dist else 0
     plans = [shard_batches(n_items, batch_size, world, r) for r in range(world)]
-    steps = plans[rank]
-    n_steps = len(steps)
+    n_steps = len(plans[rank])
     rem = gather_remainder(n_items, batch_size, world)
+    if schedule not in ("static", "dynamic"):
+        raise ValueError(f"schedule must be 'static' or 'dynamic', got {schedule!r}")
+    dynamic = schedule == "dynamic"
     if checkpoint_dir and rank == 0:
         os.makedirs(checkpoint_dir, exist_ok=True)
     dev = comm_device if comm_device is not None else (
         torch.device("cuda", torch.cuda.current_device()) if dist is not None and dist.get_backend() == "nccl"
         else torch.device("cpu"))
-    done = _done_rounds(checkpoint_dir, n_steps, dev,
-                        {"n_items": int(n_items), "batch_size": int(batch_size), "world_size": int(world),
-                         "config_sha256": digest, "gather": "end"}, rank_files=world)
+    plan = {"n_items": int(n_items), "batch_size": int(batch_size), "world_size": int(world),
+            "config_sha256": digest, "gather": "end"}
+    n_global = n_steps * world
+    if dynamic:
+        plan["schedule"] = "dynamic"
+        done = _done_rounds(checkpoint_dir, n_global, dev, plan, batch_files=True, allow_legacy=allow_legacy)
+    else:
+        done = _done_rounds(checkpoint_dir, n_steps, dev, plan, rank_files=world, allow_legacy=allow_legacy)
     decoders = decode if isinstance(decode, (list, tuple)) else [decode]
-    local: List[Optional[List[np.ndarray]]] = [None] * n_steps  # [step][column] -> (batch_size, width) int64
+    step_lock = threading.Lock()  # on_step: one call at a time, whichever lane thread finished the batch
+    # static: local[si] = the rank's step si; dynamic: mine[j] = global batch j decoded here
+    local: List[Optional[List[np.ndarray]]] = [None] * n_steps
+    mine: dict = {}
+
+    def gbatch(j):  # global batch j = round j // W, rank slot j % W of the reference's plan
+        return plans[j % world][j // world]
+
+    def report(si, total):
+        if on_step is not None:
+            with step_lock:
+                on_step(si, total)
 
     def run_step(si, dec):
         idx = steps[si]
@@ -340,57 +419,113 @@ def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, com
             if checkpoint_dir:
                 _save_round(checkpoint_dir, si, list(idx), mats, path)
         local[si] = mats
-        if on_step is not None:
-            on_step(si, n_steps)
+        report(si, n_steps)
 
-    if len(decoders) == 1:
-        for si in range(n_steps):
-            run_step(si, decoders[0])
-    else:  # lanes: step si on lane si % n (one host thread each); lane i's first step runs alone first, so every
-        # lane's graphs are captured before the threads overlap
-        n = len(decoders)
-        for si in range(min(n, n_steps)):
-            run_step(si, decoders[si])
-        errs: List[BaseException] = []
+    def run_global(j, dec):
+        idx = gbatch(j)
+        mats = [o.cpu().numpy().astype(np.int64) for o in dec(features(idx))]
+        if checkpoint_dir:
+            _save_round(checkpoint_dir, j, list(idx), mats, _batch_path(checkpoint_dir, j), rank=rank)
+        mine[j] = mats
+        report(j, n_global)
 
-        import contextlib
+    steps = plans[rank]
+    errs: List[BaseException] = []
+    import contextlib
 
-        # each lane on its own stream of this rank's device (on one shared stream the lanes would serialise; a new
-        # thread's current device is 0, the stream context sets it)
-        streams = [torch.cuda.Stream(device=torch.cuda.current_device()) for _ in range(n)] \
-            if torch.cuda.is_available() else [None] * n
+    # each lane on its own stream of this rank's device (on one shared stream the lanes would serialise; a new
+    # thread's current device is 0, the stream context sets it)
+    n = len(decoders)
+    streams = [torch.cuda.Stream(device=torch.cuda.current_device()) for _ in range(n)] \
+        if n > 1 and torch.cuda.is_available() else [None] * n
 
-        def lane_work(i):
-            try:
-                ctx = torch.cuda.stream(streams[i]) if streams[i] is not None else contextlib.nullcontext()
-                with ctx:
-                    for si in range(i + n, n_steps, n):
-                        run_step(si, decoders[i])
-            except BaseException as e:  # re-raised on the calling thread
-                errs.append(e)
+    def in_lane(i, work):
+        try:
+            ctx = torch.cuda.stream(streams[i]) if streams[i] is not None else contextlib.nullcontext()
+            with ctx:
+                work()
+        except BaseException as e:  # re-raised on the calling thread
+            errs.append(e)
 
-        threads = [threading.Thread(target=lane_work, args=(i,)) for i in range(n)]
+    def run_threads(works):
+        if len(works) == 1:
+            works[0]()
+            return
+        threads = [threading.Thread(target=in_lane, args=(i, w)) for i, w in enumerate(works)]
         for th in threads:
             th.start()
         for th in threads:
             th.join()
         if errs:
             raise errs[0]
-    for si, mats in enumerate(local):
-        if len(mats) != len(local[0]):
-            raise ValueError(f"step {si} produced {len(mats)} output columns, earlier steps {len(local[0])}")
-    n_cols = len(local[0]) if local else 0
-    if dist is not None:  # every rank runs the same number of steps (even_batches): agree on the column count
+
+    if dynamic:
+        claims = _Claims(dist, [j for j in range(n_global) if not done[j]])
+
+        def worker(dec):
+            def work():
+                while (j := claims.next()) is not None:
+                    run_global(j, dec)
+            return work
+
+        # lanes capture their graphs on their own threads (captures serialised by decode.CAPTURE_LOCK)
+        run_threads([worker(d) for d in decoders])
+    elif n == 1:
+        for si in range(n_steps):
+            run_step(si, decoders[0])
+    else:  # lanes: step si on lane si % n (one host thread each)
+        def lane_steps(i):
+            def work():
+                for si in range(i, n_steps, n):
+                    run_step(si, decoders[i])
+            return work
+
+        run_threads([lane_steps(i) for i in range(n)])
+
+    if dynamic:  # every rank's decoded batches, by global index; batches on disk read back here
+        js = sorted(mine)
+        outs = [mine[j] for j in js]
+    else:
+        outs = local
+    for k, mats in enumerate(outs):
+        if len(mats) != len(outs[0]):
+            raise ValueError(f"batch {k} produced {len(mats)} output columns, earlier batches {len(outs[0])}")
+    n_cols = len(outs[0]) if outs else 0
+    if dist is not None:  # agree on the column count (a rank may have decoded nothing)
         t = torch.tensor([n_cols], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         n_cols = int(t.item())
+    if dynamic:
+        n_cols = _dynamic_columns(n_cols, done, checkpoint_dir)
+        by_j: List[Optional[List[np.ndarray]]] = [None] * n_global
+        owner = [-1] * n_global
+        n_slots = len(js)
+        if dist is not None:
+            t = torch.tensor([n_slots], dtype=torch.int64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            n_slots = int(t.item())
+        # the global indices travel as one more matrix per rank; each column's matrices as one gather
+        idx_all = gather_matrices([np.asarray([js], dtype=np.int64).reshape(1, -1)], 1, -1, dev)
+        per_col = [gather_matrices([m[c] for m in outs], n_slots, pad_token_id, dev) for c in range(n_cols)]
+        for r in range(world):
+            for k, j in enumerate(idx_all[r][0].reshape(-1).tolist() if idx_all[r] else []):
+                by_j[j] = [per_col[c][r][k] for c in range(n_cols)]
+                owner[j] = r
+        for j in range(n_global):
+            if done[j]:
+                _, by_j[j] = _load_round(checkpoint_dir, j, _batch_path(checkpoint_dir, j))
+        _LAST_SCHEDULE = owner
+        per_rank_cols = [[[by_j[si * world + r][c] for si in range(n_steps)] for r in range(world)]
+                         for c in range(n_cols)]
+    else:
+        per_rank_cols = [gather_matrices([m[c] for m in local], n_steps, pad_token_id, dev) for c in range(n_cols)]
     eval_ids: List[int] = []
     for si in range(n_steps):
         fid = [i for r in range(world) for i in plans[r][si]]
         eval_ids.extend(fid[:rem] if si == n_steps - 1 and rem > 0 else fid)
     cols: List[List[np.ndarray]] = []
     for c in range(n_cols):
-        per_rank = gather_matrices([m[c] for m in local], n_steps, pad_token_id, dev)
+        per_rank = per_rank_cols[c]
         out: List[np.ndarray] = []
         for si in range(n_steps):
             w = max(per_rank[r][si].shape[1] for r in range(world))  # the round's common width
@@ -406,6 +541,14 @@ def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, com
             out.extend(mat)
         cols.append(out)
     return eval_ids, cols
+
+
+def _dynamic_columns(n_cols: int, done: List[bool], checkpoint_dir: Optional[str]) -> int:
+    """Output columns when no rank decoded anything this run (every batch resumed from disk)."""
+    if n_cols or not any(done):
+        return n_cols
+    j = done.index(True)
+    return len(_load_round(checkpoint_dir, j, _batch_path(checkpoint_dir, j))[1])
 
 
 def gather_matrices(mats: Sequence[np.ndarray], n_slots: int, pad: int, device=None) -> List[List[np.ndarray]]:
@@ -468,7 +611,8 @@ def _loop(gather):
 def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_items: int, *, batch_size: int,
                  pad_token_id: int, gen_kwargs: Optional[dict] = None, comm_device=None,
                  on_step: Optional[Callable[[int, int], None]] = None, legacy_prompt_in_output: bool = False,
-                 checkpoint_dir: Optional[str] = None, gather: str = "round", lanes: int = 1):
+                 checkpoint_dir: Optional[str] = None, gather: str = "round", lanes: int = 1,
+                 schedule: str = "static", allow_legacy_checkpoint: bool = False):
     """Transcribe items 0..n_items-1 data-parallel; returns (item_indices, predictions) in dataset order
     on every rank (``run_pseudo_labelling.py:333-344``).
 
@@ -486,7 +630,11 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
     ``lanes`` > 1 (with gather="end"): that many of the rank's batches decode at once, each batch still
     ``batch_size`` items, on ``model.lane()`` handles (shared weights, one host thread and stream each): one
     batch's latency-bound decode chain overlaps another's HBM-bound cross-attention (tools/lab/dual_decode.py).
-    The predictions are the same."""
+    ``schedule`` (with gather="end"): "static" = accelerate's batch-to-rank plan; "dynamic" = the same batches, each
+    taken by the first idle worker of any rank (``_label_loop_deferred``).  The predictions are the same.
+    ``on_step(step, total)`` runs on the thread that decoded the step (a lane thread with lanes > 1), one call at a
+    time, in completion order.  ``allow_legacy_checkpoint``: resume a ``checkpoint_dir`` whose plan.json predates
+    the configuration digest (refused by default)."""
     gen_kwargs = dict(gen_kwargs or {})
     loop = _loop(gather)
     models = _lane_models(model, lanes, gather)
@@ -509,7 +657,8 @@ def pseudo_label(model, features: Callable[[Sequence[int]], torch.Tensor], n_ite
                         legacy_prompt_in_output=bool(legacy_prompt_in_output)) if checkpoint_dir else None
     decs = [decoder(m) for m in models]
     eval_ids, cols = loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step,
-                          decs if len(decs) > 1 else decs[0], checkpoint_dir, digest)
+                          decs if len(decs) > 1 else decs[0], checkpoint_dir, digest, schedule=schedule,
+                          allow_legacy=allow_legacy_checkpoint)
     return eval_ids, (cols[0] if cols else [])
 
 
@@ -517,7 +666,7 @@ def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tens
                            batch_size: int, text_lang_task: Sequence[tuple], pad_token_id: int,
                            gen_kwargs: Optional[dict] = None, comm_device=None,
                            on_step: Optional[Callable[[int, int], None]] = None, checkpoint_dir: Optional[str] = None,
-                           gather: str = "round"):
+                           gather: str = "round", schedule: str = "static", allow_legacy_checkpoint: bool = False):
     """``run_pseudo_labelling_v3.py:299-321``: every batch is decoded once per (text, lang, task) triple.
     Returns (item_indices, {text: predictions}) in dataset order; ``whisper_<text>`` is the column the
     reference adds (:322-323).  The encoder and cross-K/V run once per batch (``generate_multitask``) when
@@ -534,7 +683,7 @@ def pseudo_label_multitask(model, features: Callable[[Sequence[int]], torch.Tens
     digest = run_digest(model, gen_kwargs=gen_kwargs, pad_token_id=int(pad_token_id),
                         text_lang_task=[list(t) for t in text_lang_task]) if checkpoint_dir else None
     eval_ids, cols = loop(model, features, n_items, batch_size, pad_token_id, comm_device, on_step, decode,
-                          checkpoint_dir, digest)
+                          checkpoint_dir, digest, schedule=schedule, allow_legacy=allow_legacy_checkpoint)
     if not cols:
         cols = [[] for _ in text_lang_task]
     return eval_ids, {t[0]: c for t, c in zip(text_lang_task, cols)}

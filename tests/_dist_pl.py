@@ -52,7 +52,7 @@ def main():
 
     clips = [{"array": reazon_audio(50 + i, 40.0 - 9 * i), "sampling_rate": 16000} for i in range(3)]
     kwp = dict(chunk_length_s=15, batch_size=2, generate_kwargs=dict(language="ja", task="transcribe", max_length=32))
-    dp = ASRPipeline(model, **kwp)(clips, return_timestamps=True)
+    dp = ASRPipeline(model, data_parallel=True, **kwp)(clips, return_timestamps=True)
     single = ASRPipeline(model, data_parallel=False, **kwp)(clips, return_timestamps=True)
     out["pipeline"] = json.dumps(dp, default=str) == json.dumps(single, default=str)
     dist.barrier()

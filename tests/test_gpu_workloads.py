@@ -178,9 +178,21 @@ def test_config3_fp32_generate_b32_bitexact(large_b32_gold):
     mode: exact-fp32 MFMA GEMMs, separate LayerNorms)."""
     g, feats_np = large_b32_gold
     model = _model(LARGE_V3, torch.float32)
-    toks = model.generate(torch.from_numpy(feats_np).cuda(), language="ja", task="transcribe", max_length=128)
+    feats = torch.from_numpy(feats_np).cuda()
+    toks = model.generate(feats, language="ja", task="transcribe", max_length=128)
     np.testing.assert_array_equal(toks.cpu().numpy(), g["greedy_tokens"])
-    del model
+    # north star: logits within 1e-3 of the HF fp32 reference -- teacher-forced along transformers' own greedy
+    # sequence, at its top-8 ids of every one of the 124 steps of all 32 rows (raw logits, utils.py:2894)
+    eng = model.engine
+    sess = eng.new_session(32, eng.encode(feats))
+    lg = sess.teacher_forced_logits(torch.from_numpy(g["greedy_sequences"])[:, :-1], 4)
+    idx = torch.from_numpy(g["greedy_logits_top_idx"].astype(np.int64)).cuda()
+    got = torch.gather(lg[:, : idx.shape[1]], -1, idx).cpu().numpy()
+    err = np.abs(got - g["greedy_logits_top_val"])
+    print(f"\nconfig3 fp32 teacher-forced logits vs HF fp32 over {err.size} values: max {err.max():.2e} mean "
+          f"{err.mean():.2e} (|logit| max {np.abs(g['greedy_logits_top_val']).max():.2f})")
+    np.testing.assert_allclose(got, g["greedy_logits_top_val"], atol=1e-3, rtol=0)
+    del model, sess, lg
     _free()
 
 

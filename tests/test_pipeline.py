@@ -250,7 +250,8 @@ def _dp_pipe_worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         m = _StubASRModel()
-        got = ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2)(_dp_clips())
+        got = ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2,
+                          data_parallel=True)(_dp_clips())
         with open(os.path.join(out_dir, f"p{rank}.json"), "w") as f:
             json.dump({"res": got, "calls": m.calls}, f, default=lambda x: x.tolist() if hasattr(x, "tolist") else x)
     finally:
@@ -281,6 +282,44 @@ def test_pipeline_data_parallel_gloo_matches_single_process(tmp_path, world):
         assert z["res"] == want
         calls.append(z["calls"])
     assert sum(calls) == m1.calls and max(calls) - min(calls) <= 1
+
+
+def _dp_mismatch_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+
+    from kwhisper.pipeline import ASRPipeline
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        clips = _dp_clips()
+        if rank == 1:  # a per-rank shard of the inputs: another clip in position 2 (same window count)
+            clips[2] = {"array": clips[2]["array"][::-1].copy(), "sampling_rate": 16000}
+        msg, m = "", _StubASRModel()
+        try:
+            ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2, data_parallel=True)(clips)
+        except ValueError as e:
+            msg = str(e)
+        # data_parallel off (the default): each rank decodes its own inputs, no collective
+        ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2)(clips)
+        with open(os.path.join(out_dir, f"m{rank}.txt"), "w") as f:
+            f.write(msg)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_pipeline_data_parallel_refuses_different_inputs(tmp_path):
+    """data_parallel is opt-in, and with it every rank must pass the same inputs -- ranks holding
+    different audio raise ValueError on every rank (before any window batch is split or gathered)."""
+    import socket
+
+    import torch.multiprocessing as mp
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_dp_mismatch_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert "same inputs on every rank" in open(tmp_path / f"m{r}.txt").read()
 
 
 class _LaneASRModel(_StubASRModel):
@@ -327,7 +366,8 @@ def _dp_lanes_worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         m = _LaneASRModel()
-        got = ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=1, lanes=2)(_dp_clips())
+        got = ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=1, lanes=2,
+                          data_parallel=True)(_dp_clips())
         with open(os.path.join(out_dir, f"l{rank}.json"), "w") as f:
             json.dump({"res": got, "calls": sum(h.calls for h in m.handles)}, f,
                       default=lambda x: x.tolist() if hasattr(x, "tolist") else x)

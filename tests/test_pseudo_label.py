@@ -382,9 +382,10 @@ def test_deferred_gather_resume_gloo_world2(tmp_path):
         assert b["decoded"].tolist() == [[8, 9], [10, 11]][r]
 
 
-def test_resume_accepts_legacy_plan_without_digest(tmp_path):
-    """A checkpoint directory written before plan.json carried config_sha256 resumes (with a warning) instead of
-    being refused as another plan."""
+def test_resume_refuses_legacy_plan_unless_allowed(tmp_path):
+    """A checkpoint directory written before plan.json carried config_sha256 cannot prove its rounds were decoded
+    with this run's generate kwargs and weights: refused by default, resumed (with a warning) only with
+    allow_legacy_checkpoint=True."""
     import json
 
     ck = tmp_path / "ck"
@@ -393,8 +394,11 @@ def test_resume_accepts_legacy_plan_without_digest(tmp_path):
     plan.pop("config_sha256")
     (ck / "plan.json").write_text(json.dumps(plan))
     m = _CountingModel()
+    with pytest.raises(ValueError, match="allow_legacy_checkpoint"):
+        pseudo_label(m, _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=str(ck))
     with pytest.warns(RuntimeWarning, match="predates"):
-        got = pseudo_label(m, _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=str(ck))
+        got = pseudo_label(m, _features, 10, batch_size=4, pad_token_id=PAD, checkpoint_dir=str(ck),
+                           allow_legacy_checkpoint=True)
     _same(got, ref)
     assert m.batches == []
 
@@ -457,3 +461,135 @@ def test_lanes_checkpoint_resume(tmp_path):
                         checkpoint_dir=str(ck))
     _same(part, ref)
     assert sum(len(h.batches) for h in m3.lanes) == len(victims)
+
+
+# ---- dynamic batch assignment (schedule="dynamic": list scheduling over a shared counter) -----
+class _SlowModel(_CountingModel):
+    """Batches holding an item of ``slow`` take ``delay`` seconds (a batch with extra seek passes)."""
+
+    def __init__(self, slow=(), delay=0.0):
+        super().__init__()
+        self.slow, self.delay = set(slow), delay
+
+    def generate(self, feats, **kw):
+        import time
+
+        if self.slow & set(feats[:, 0].long().tolist()):
+            time.sleep(self.delay)
+        return super().generate(feats, **kw)
+
+
+def _dynamic_worker(rank, world, port, n, bs, out_dir, ck, slow, lanes):
+    import json
+
+    import torch.distributed as dist
+
+    from kwhisper.pseudo_label import last_schedule
+
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        ref = pseudo_label(_StubModel(), _features, n, batch_size=bs, pad_token_id=PAD)  # per-round, static
+        m = _SlowModel(slow if rank == 0 else (), 0.4)
+        if lanes > 1:
+            m = _LaneStub()
+        got = pseudo_label(m, _features, n, batch_size=bs, pad_token_id=PAD, gather="end", schedule="dynamic",
+                           checkpoint_dir=ck or None, lanes=lanes)
+        handles = m.lanes if lanes > 1 else [m]
+        with open(os.path.join(out_dir, f"y{rank}.json"), "w") as f:
+            json.dump({"same": got[0] == ref[0] and len(got[1]) == len(ref[1])
+                       and all(np.array_equal(a, b) for a, b in zip(got[1], ref[1])),
+                       "decoded": [b for h in handles for b in h.batches], "schedule": last_schedule()}, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,bs,world,lanes", [(13, 2, 2, 1), (23, 3, 3, 1), (40, 4, 2, 2), (3, 4, 2, 1)])
+def test_dynamic_schedule_gloo_equals_static(tmp_path, n, bs, world, lanes):
+    """schedule="dynamic" under gloo world 2 / 3 (and with two lanes per rank): every rank returns exactly the
+    reference's per-round gather (items, order, each row padded to its round's widest batch, wrapped duplicates
+    dropped); every batch of the static plan is decoded exactly once, by the rank last_schedule() names."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    mp.spawn(_dynamic_worker, args=(world, _free_port(), n, bs, str(tmp_path), "", (), lanes), nprocs=world,
+             join=True)
+    want = {tuple(b) for r in range(world) for b in shard_batches(n, bs, world, r)}
+    runs = [json.load(open(tmp_path / f"y{r}.json")) for r in range(world)]
+    decoded = [tuple(b) for z in runs for b in z["decoded"]]
+    assert all(z["same"] for z in runs)
+    assert sorted(decoded) == sorted(want) and len(decoded) == len(want)
+    plans = [shard_batches(n, bs, world, r) for r in range(world)]
+    for z in runs:
+        assert z["schedule"] == runs[0]["schedule"]
+        for j, r in enumerate(z["schedule"]):  # global batch j = round j // W, rank slot j % W
+            assert plans[j % world][j // world] in runs[r]["decoded"]
+
+
+def test_dynamic_schedule_balances_a_slow_rank(tmp_path):
+    """Rank 0 draws a slow batch (0.4 s, as a three-pass batch costs twice a one-pass one): under the static plan it
+    would still decode half of the batches; with dynamic claims rank 1 takes the batches rank 0 is not ready for."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    n, bs = 16, 2  # 8 batches
+    mp.spawn(_dynamic_worker, args=(2, _free_port(), n, bs, str(tmp_path), "", (0,), 1), nprocs=2, join=True)
+    runs = [json.load(open(tmp_path / f"y{r}.json")) for r in range(2)]
+    assert all(z["same"] for z in runs)
+    assert len(runs[1]["decoded"]) >= 5, runs  # rank 0 spent 0.4 s on batch 0: rank 1 took (nearly) all the rest
+
+
+def test_dynamic_schedule_resume_gloo_world2(tmp_path):
+    """Dynamic resume: one file per global batch (with the rank that decoded it); after two files are lost the rerun
+    decodes exactly those two batches (whichever rank claims them) and returns the same predictions."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    n, bs = 13, 2
+    ck = str(tmp_path / "ck")
+    mp.spawn(_dynamic_worker, args=(2, _free_port(), n, bs, str(tmp_path), ck, (), 1), nprocs=2, join=True)
+    files = sorted(f for f in os.listdir(ck) if f.endswith(".npz"))
+    assert files == [f"batch_{j:06d}.npz" for j in range(8)]
+    first = [json.load(open(tmp_path / f"y{r}.json")) for r in range(2)]
+    for j in range(8):
+        with np.load(os.path.join(ck, files[j])) as z:
+            assert int(z["rank"]) == first[0]["schedule"][j]
+    os.remove(os.path.join(ck, files[2]))
+    os.remove(os.path.join(ck, files[7]))
+    mp.spawn(_dynamic_worker, args=(2, _free_port(), n, bs, str(tmp_path), ck, (), 1), nprocs=2, join=True)
+    runs = [json.load(open(tmp_path / f"y{r}.json")) for r in range(2)]
+    assert all(z["same"] for z in runs)
+    plans = [shard_batches(n, bs, 2, r) for r in range(2)]
+    redone = sorted(tuple(b) for z in runs for b in z["decoded"])
+    assert redone == sorted([tuple(plans[0][1]), tuple(plans[1][3])])  # global batches 2 and 7
+    assert [x for x in runs[0]["schedule"] if x >= 0] and runs[0]["schedule"].count(-1) == 6
+
+
+@pytest.mark.parametrize("lanes", [1, 2, 3])
+def test_dynamic_schedule_single_process(lanes):
+    """Without a process group the claims come from a local counter shared by the lanes: same predictions as the
+    static plan, every batch once; on_step sees every global batch once, one call at a time."""
+    import threading
+
+    ref = pseudo_label(_StubModel(), _features, 23, batch_size=4, pad_token_id=PAD, gather="end")
+    m = _LaneStub()
+    seen, busy, clash = [], threading.Lock(), []
+
+    def on_step(j, total):
+        if not busy.acquire(blocking=False):
+            clash.append(j)
+            return
+        try:
+            seen.append((j, total))
+        finally:
+            busy.release()
+
+    got = pseudo_label(m, _features, 23, batch_size=4, pad_token_id=PAD, gather="end", schedule="dynamic",
+                       lanes=lanes, on_step=on_step)
+    _same(got, ref)
+    assert sorted(seen) == [(j, 6) for j in range(6)] and not clash
+    assert sorted(tuple(b) for h in m.lanes for b in h.batches) == sorted(tuple(b) for b in shard_batches(23, 4, 1, 0))
+    with pytest.raises(ValueError, match="schedule"):
+        pseudo_label(_StubModel(), _features, 3, batch_size=4, pad_token_id=PAD, schedule="dynamic")

@@ -91,7 +91,7 @@ def config4(a, world, rank, dev):
     t0 = time.perf_counter()
     ids, preds = pseudo_label(model, features, n, batch_size=a.batch, gen_kwargs=gen_kw, gather=a.gather,
                               pad_token_id=model.generation_config.eos_token_id,  # tokenizer pad = <|endoftext|>
-                              on_step=on_step, lanes=a.lanes)
+                              on_step=on_step, lanes=a.lanes, schedule=a.schedule)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -105,26 +105,39 @@ def config4(a, world, rank, dev):
             "dtype": "bf16", "data": "synthetic (ReazonSpeech-tiny duration statistics, noise audio, random weights)",
             "config": {"workload": "config 4: run_pseudo_labelling.py loop, whisper-large-v3, timestamps, greedy",
                        "per_gpu_batch": a.batch, "max_length": a.max_length, "parallelism": f"dp{world}",
-                       "gather": a.gather, "lanes": a.lanes,
+                       "gather": a.gather, "lanes": a.lanes, "schedule": a.schedule,
                        "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))},
             "batch_seconds": [round(float(x), 5) for x in batch_s], "batch_seek_passes": [passes[si] for si in sorted(passes)],
             "dp_projection": dp_projection(batch_s) if world == 1 and a.lanes == 1 else None}
 
 
 def dp_projection(batch_s, worlds=(2, 4, 8)):
-    """Projected data-parallel efficiency at W ranks from W = 1 per-batch times.  Global batch
-    i runs on rank i % W (accelerate's shard plan; the wrapped duplicates of the last round are real work).
-    Lock step (the reference's per-batch gather, gather="round"): every round waits for its slowest batch,
-    efficiency = sum over rounds of the mean batch time / sum of the max.  Deferred (gather="end"): ranks run
-    free until one exchange, efficiency = (total / W) / the busiest rank's sum."""
+    """Projected data-parallel efficiency at W ranks from W = 1 per-batch times.
+    Global batch i runs on rank i % W (accelerate's shard plan; the wrapped duplicates of the last round are real
+    work).  Lock step (the reference's per-batch gather, gather="round"): every round waits for its slowest batch,
+    efficiency = sum over rounds of the mean batch time / sum of the max.  Deferred (gather="end", schedule static):
+    ranks run free until one exchange, efficiency = (total / W) / the busiest rank's sum.  Dynamic (gather="end",
+    schedule="dynamic"): the batches in plan order, each to the first idle rank (list scheduling), efficiency =
+    (total / W) / the last rank's finish.  ``dynamic_x10``: the same, over ten copies of these batch times (a shard
+    ten times the stand-in's 56 batches): at 7 batches per rank the job's tail -- the last claimed batch's seek
+    passes, which no claim order known in advance can move earlier -- is a large part of each rank's share."""
+    import heapq
+
     t = np.asarray(batch_s, dtype=np.float64)
     out = {}
     for W in worlds:
         n_rounds = -(-len(t) // W)
         tt = np.concatenate([t, t[: n_rounds * W - len(t)]]) if n_rounds * W > len(t) else t  # wrap-around
         r = tt.reshape(n_rounds, W)
+        def listed(x):
+            free = [0.0] * W
+            for v in x:  # list scheduling: the next batch to the rank that frees first
+                heapq.heapreplace(free, free[0] + v)
+            return float(x.sum() / W / max(free))
+
         out[f"w{W}"] = {"lockstep": round(float(r.mean(1).sum() / r.max(1).sum()), 4),
-                        "deferred": round(float(r.sum() / W / r.sum(0).max()), 4)}
+                        "deferred": round(float(tt.sum() / W / r.sum(0).max()), 4),
+                        "dynamic": round(listed(tt), 4), "dynamic_x10": round(listed(np.tile(t, 10)), 4)}
     return out
 
 
@@ -140,7 +153,7 @@ def config5(a, world, rank, dev):
     del sd
     # W > 1: the pipeline's window batches go round-robin over the ranks (ASRPipeline.data_parallel), one
     # gather of the token matrices at the end; every rank merges the full result
-    pipe = ASRPipeline(model, chunk_length_s=15, batch_size=a.batch, lanes=a.lanes,
+    pipe = ASRPipeline(model, chunk_length_s=15, batch_size=a.batch, lanes=a.lanes, data_parallel=True,
                        generate_kwargs=dict(language="ja", task="transcribe", num_beams=5, max_length=a.max_length))
     clips = [{"array": clip_audio(i, 30.0), "sampling_rate": SR} for i in range(a.clips)]
     # warm-up (graph capture on every lane), no collective: one window batch per lane (3 windows per 30 s clip)
@@ -179,6 +192,9 @@ def main():
     ap.add_argument("--max-length", type=int, default=128)
     ap.add_argument("--gather", choices=("round", "end"), default="end",
                     help="config 4: the reference's per-batch gather (round) or one exchange at the end")
+    ap.add_argument("--schedule", choices=("static", "dynamic"), default="dynamic",
+                    help="config 4 with --gather end: accelerate's batch-to-rank plan, or each batch to the first idle "
+                    "rank (pseudo_label schedule='dynamic'; the same outputs)")
     ap.add_argument("--lanes", type=int, default=1,
                     help="batches of --batch in flight per GPU (config 4: pseudo_label lanes, needs --gather end; "
                     "config 5: ASRPipeline lanes)")
