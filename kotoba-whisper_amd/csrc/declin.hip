@@ -894,22 +894,35 @@ __global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
 // weight stream: the generic kernel above re-reads the 32 activation rows from L2 in every one of its
 // 1,621 workgroups (as many L2 bytes as weight bytes) and runs 1.6 rounds of them.  Here each of
 // ~256 workgroups loads its waves' activation fragments and the rows' LayerNorm statistics ONCE, then
-// walks a contiguous run of column groups (2 x 16 columns each) with the next group's weights in
+// walks a contiguous run of column groups (2 x 16 columns each) with the NEXT TWO groups' weights in
 // flight while the current one is reduced across waves and written (fixed-order sums: deterministic).
+// r05: the epilogue's column sums / biases of the whole run are staged in LDS at the start (no
+// epilogue load in the loop), each prefetch is pinned where it is written (sched_barrier: the scheduler had sunk
+// the next group's loads below the current group's waits), and the per-group barrier is a raw s_barrier after an
+// LDS-only wait (__syncthreads drained every load in flight, the prefetch included).
 #ifndef KW_LMH_MAX_ROWS
 #define KW_LMH_MAX_ROWS 32  // (lab knob: rows up to which the LM head takes lm_head_kernel)
 #endif
 constexpr int LMH_KTM = 5;   // k-tiles per wave
 constexpr int LMH_NCB = 2;   // column blocks per group
+constexpr int LMH_MAXG = 16; // column groups per workgroup (epilogue constants staged in LDS; host-checked)
+#ifndef KW_LMH_BUFS
+#define KW_LMH_BUFS 3  // weight groups in registers: two in flight beside the one being multiplied (2: one)
+#endif
+
+__device__ __forceinline__ void lmh_barrier() {  // LDS writes visible, then s_barrier: global loads stay in flight
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 
 __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg) {
   DecP p = p0;  // blockIdx.z = 32-row chunk (beam rows), as in dec_linear_kernel
   p.M = min(32, p0.M - 32 * (int)blockIdx.z);
   p.x += (int64_t)32 * blockIdx.z * p0.ldx;
   p.C = reinterpret_cast<float*>(p0.C) + (int64_t)32 * blockIdx.z * p0.ldc;
-  __shared__ f32x4 red[2][MAXW][LMH_NCB][2][64];  // double-buffered per-wave partial tiles
+  __shared__ f32x4 red[3][MAXW][LMH_NCB][2][64];  // per-wave partial tiles, one slot per group in flight
   __shared__ float rpart[MAXW][32][2];
   __shared__ float rstat[32][2];
+  __shared__ float econ[LMH_MAXG][LMH_NCB][2][16];  // [group][column block][colsum, bias][column]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int nkt = p.K >> 5;
   const int kt0 = (nkt * wave) / nw, kt1 = (nkt * (wave + 1)) / nw;  // <= LMH_KTM (host-checked)
@@ -918,24 +931,32 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   const int n_groups = (p.N + 16 * LMH_NCB - 1) / (16 * LMH_NCB);
   const int g0 = blockIdx.x * groups_per_wg, g1 = min(n_groups, g0 + groups_per_wg);
   if (g0 >= g1) return;
-  const int n_cb = (p.N + 15) / 16;
-  // a group's weights AND the column sum / bias its epilogue waves (0..2*NCB-1) need, in one batch: an
-  // epilogue load issued after the next group's prefetch waits for that prefetch too (vmcnt is in order)
-  auto wload = [&](int g, bf16x8 (&w)[LMH_NCB][LMH_KTM], float& ecs, float& ebn) {
+  // the run's weights through a bounds-checked buffer resource: a prefetch past the run (g >= g1) returns zeros
+  // without a memory access, so every prefetch is unconditional (a conditional load made the compiler's wait counts
+  // at the loop's joins assume it absent -- and wait for every load in flight).  The packed matrix pads N to 32
+  // columns, so each of the run's groups has both column blocks.
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16x8*>(p.W) + (int64_t)g0 * LMH_NCB * nkt * 64, (short)0, (g1 - g0) * LMH_NCB * nkt * 1024, 0x00020000);
+  auto wload = [&](int g, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
 #pragma unroll
-    for (int c = 0; c < LMH_NCB; ++c) {
-      const int cb = min(g * LMH_NCB + c, n_cb - 1);
+    for (int c = 0; c < LMH_NCB; ++c)
 #pragma unroll
       for (int u = 0; u < LMH_KTM; ++u)
-        w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)cb * nkt + min(kt0 + u, ktl)) * 64 + lane);
-    }
-    const int n = min((g * LMH_NCB + ((wave >> 1) & (LMH_NCB - 1))) * 16 + (lane & 15), p.N - 1);
-    ecs = p.ln_colsum[n];
-    ebn = p.bias ? p.bias[n] : 0.f;
+        w[c][u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   wrs, (((g - g0) * LMH_NCB + c) * nkt + min(kt0 + u, ktl)) * 1024 + lane * 16,
+                                                   0, 2));  // aux 2 = nt
+    __builtin_amdgcn_sched_barrier(0);  // the loads stay here, ahead of the waits for earlier groups
   };
-  bf16x8 wa[LMH_NCB][LMH_KTM], wb[LMH_NCB][LMH_KTM];
-  float csa, bna, csb, bnb;
-  wload(g0, wa, csa, bna);
+  // issue order = wait order (vmcnt retires in order): the epilogue constants and the activation fragments first,
+  // then the first two groups' weights, so the LayerNorm phase waits on the activations alone
+  const int ncon = (g1 - g0) * LMH_NCB * 16;  // this run's columns: thread t < ncon stages column t
+  float con_cs, con_bn;
+  {
+    const int t = min(tid, ncon - 1);
+    const int n = min(g0 * LMH_NCB * 16 + t, p.N - 1);
+    con_cs = p.ln_colsum[n];
+    con_bn = p.bias ? p.bias[n] : 0.f;
+  }
   // activation fragments of this wave's k-range, once (rows lane&15 and 16 + lane&15)
   bf16x8 a0[LMH_KTM], a1[LMH_KTM];
   {
@@ -946,6 +967,26 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       a0[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r0 * p.ldx + k);
       a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
     }
+  }
+  bf16x8 wa[LMH_NCB][LMH_KTM], wb[LMH_NCB][LMH_KTM];
+#if KW_LMH_BUFS == 3
+  bf16x8 wc[LMH_NCB][LMH_KTM];
+#endif
+  wload(g0, wa);
+  wload(g0 + 1, wb);
+  if (tid < ncon) {
+    const int gi = tid / (LMH_NCB * 16), c = (tid / 16) % LMH_NCB, col = tid % 16;
+    econ[gi][c][0][col] = con_cs;
+    econ[gi][c][1][col] = con_bn;
+  }
+  // a wave with fewer than LMH_KTM k-tiles multiplies zero activations for the rest (exact: 0 x w adds +0), so the
+  // loop's MFMAs carry no per-k-tile branch (whose joins made the compiler wait for every load in flight)
+  bf16x8 za0[LMH_KTM], za1[LMH_KTM];
+#pragma unroll
+  for (int u = 0; u < LMH_KTM; ++u) {
+    const bool in = kt0 + u < kt1;
+    za0[u] = in ? a0[u] : bf16x8{};
+    za1[u] = in ? a1[u] : bf16x8{};
   }
   // LayerNorm statistics of the 32 rows on the matrix cores (as dec_linear_kernel step 3)
   {
@@ -973,7 +1014,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       rpart[wave][lane & 15][1] = q0[di];
       rpart[wave][16 + (lane & 15)][1] = q1[di];
     }
-    __syncthreads();
+    __syncthreads();  // (also the epilogue constants: loaded before it)
     if (tid < 32) {
       float sx = 0.f, sq = 0.f;
       for (int w2 = 0; w2 < nw; ++w2) {
@@ -985,52 +1026,64 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       rstat[tid][0] = mean;
       rstat[tid][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + p.ln_eps);
     }
+    __syncthreads();
   }
-  // walk the run: weights of group g+1 in flight while group g is multiplied, reduced and stored
-  auto body = [&](int g, int par, bf16x8 (&w)[LMH_NCB][LMH_KTM], float cs, float bn) {
+  // walk the run: groups g+1 and g+2 in flight while group g is multiplied, reduced and stored
+  auto body = [&](int g, int slot, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
     f32x4 c0[LMH_NCB], c1[LMH_NCB];
 #pragma unroll
     for (int c = 0; c < LMH_NCB; ++c) {
       c0[c] = f32x4{0.f, 0.f, 0.f, 0.f};
       c1[c] = c0[c];
 #pragma unroll
-      for (int u = 0; u < LMH_KTM; ++u)
-        if (kt0 + u < kt1) {
-          c0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0[u], w[c][u], c0[c], 0, 0, 0);
-          c1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1[u], w[c][u], c1[c], 0, 0, 0);
-        }
-      red[par][wave][c][0][lane] = c0[c];
-      red[par][wave][c][1][lane] = c1[c];
+      for (int u = 0; u < LMH_KTM; ++u) {
+        c0[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(za0[u], w[c][u], c0[c], 0, 0, 0);
+        c1[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(za1[u], w[c][u], c1[c], 0, 0, 0);
+      }
+      red[slot][wave][c][0][lane] = c0[c];
+      red[slot][wave][c][1][lane] = c1[c];
     }
-    __syncthreads();  // (double-buffered red: the next group's writes go to the other half)
+    lmh_barrier();  // (three red slots: a slot is rewritten two barriers after its readers passed)
     // waves 0..2*NCB-1 each finish one 16 x 16 tile: wave-ordered sum, LayerNorm, bias, store
     if (wave < 2 * LMH_NCB) {
       const int c = wave >> 1, hh = wave & 1;
-      f32x4 acc = red[par][0][c][hh][lane];
-      for (int w2 = 1; w2 < nw; ++w2) acc += red[par][w2][c][hh][lane];
+      f32x4 acc = red[slot][0][c][hh][lane];
+      for (int w2 = 1; w2 < nw; ++w2) acc += red[slot][w2][c][hh][lane];
       const int n = (g * LMH_NCB + c) * 16 + (lane & 15);
+      const float cs = econ[g - g0][c][0][lane & 15], bn = econ[g - g0][c][1][lane & 15];
       if (n < p.N) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = 16 * hh + 4 * (lane >> 4) + r;
           if (m < M) {
             const float v = rstat[m][1] * (acc[r] - rstat[m][0] * cs) + bn;
-            reinterpret_cast<float*>(p.C)[(int64_t)m * p.ldc + n] = v;
+            __builtin_nontemporal_store(v, reinterpret_cast<float*>(p.C) + (int64_t)m * p.ldc + n);
           }
         }
       }
     }
   };
-  int par = 0;
-  for (int g = g0; g < g1; g += 2) {
-    if (g + 1 < g1) wload(g + 1, wb, csb, bnb);
-    body(g, par, wa, csa, bna);
-    par ^= 1;
-    if (g + 1 >= g1) break;
-    if (g + 2 < g1) wload(g + 2, wa, csa, bna);
-    body(g + 1, par, wb, csb, bnb);
-    par ^= 1;
+#if KW_LMH_BUFS == 3
+  int g = g0;
+  for (; g + 2 < g1; g += 3) {
+    wload(g + 2, wc);
+    body(g, 0, wa);
+    wload(g + 3, wa);
+    body(g + 1, 1, wb);
+    wload(g + 4, wb);
+    body(g + 2, 2, wc);
   }
+  if (g < g1) body(g, 0, wa);
+  if (g + 1 < g1) body(g + 1, 1, wb);
+#else
+  for (int g = g0 + 1; g < g1; g += 2) {  // (group g0 + 1 is already in flight)
+    body(g - 1, 0, wa);
+    wload(g + 1, wa);
+    body(g, 1, wb);
+    wload(g + 2, wb);
+  }
+  if ((g1 - g0) & 1) body(g1 - 1, 0, wa);
+#endif
 }
 
 __global__ void pack_kernel(const bf16_t* __restrict__ W, int N, int K, bf16_t* __restrict__ out) {
@@ -1190,6 +1243,19 @@ hipError_t launch(const DecP& p, bool resid, const Geo& g, bool c_f32, hipStream
   return g.ncb == 2 ? launch_k<10, 2>(p, resid, g, c_f32, s) : launch_k<10, 1>(p, resid, g, c_f32, s);
 }
 
+// the LM head's column groups per workgroup: one run per CU
+int lmh_groups_per_wg(int64_t N) {
+  static int ncu = 0;
+  if (!ncu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        ncu <= 0)
+      ncu = 256;
+  }
+  const int groups = (int)((N + 16 * LMH_NCB - 1) / (16 * LMH_NCB));
+  return (groups + ncu - 1) / ncu;
+}
+
 }  // namespace
 
 extern "C" size_t kw_dec_linear_workspace_bytes(int64_t N, int64_t K) {
@@ -1255,7 +1321,8 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? KW_OK : kw_set_error(e);
   }
-  const bool lmh = lm_shape && (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && a->M <= KW_LMH_MAX_ROWS;
+  const bool lmh = lm_shape && (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && a->M <= KW_LMH_MAX_ROWS &&
+                   lmh_groups_per_wg(a->N) <= LMH_MAXG;
   // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each)
   const int64_t step = (g.ks == 1 || lmh) ? a->M : 32 * ZMAX;
   for (int64_t m0 = 0; m0 < a->M; m0 += step) {
@@ -1283,15 +1350,8 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     p.slab = a->workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(a->workspace) + CNT_MAX * sizeof(int)) : nullptr;
     p.xlds = use_xlds(a->N, g) ? 1 : 0;
     if (lmh) {
-      static int ncu = 0;
-      if (!ncu) {
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            ncu <= 0)
-          ncu = 256;
-      }
       const int groups = (int)((a->N + 16 * LMH_NCB - 1) / (16 * LMH_NCB));
-      const int per = (groups + ncu - 1) / ncu;
+      const int per = lmh_groups_per_wg(a->N);
       const int nwv = (nkt + LMH_KTM - 1) / LMH_KTM;
       hipLaunchKernelGGL(lm_head_kernel, dim3((unsigned)((groups + per - 1) / per), 1, (unsigned)((p.M + 31) / 32)),
                          dim3((unsigned)(64 * nwv)), 0, s, p, per);

@@ -522,9 +522,9 @@ def _c4_features(g):
     return torch.from_numpy(log_mel(np.stack(clips), LARGE_V3.num_mel_bins)).cuda()
 
 
-# the first 32 stand-in clips (every row one seek pass).  No stand-in clip takes a second pass under transformers'
-# fp32 large-v3 (profiles/r04d_multipass_scan.json), so tools/make_fixtures.py --only large_c4_mp has nothing to
-# write; the multi-pass path is pinned at large-v3 by test_large_v3_longform_multipass instead (10 rows).
+# the first 32 stand-in clips (every row one seek pass on the oracle log-mel: no stand-in clip takes a second pass
+# under transformers' fp32 large-v3 there, profiles/r04d_multipass_scan.json).  The multi-pass case on the product's
+# own HIP log-mel is pinned by test_config4_hipmel_multipass (tests/golden/large_v3_c4_hipmel.npz).
 C4_FIXTURES = ["large_v3_ts_b32_fp32"]
 
 
@@ -556,9 +556,6 @@ def test_config4_fp32_pseudo_label_bitexact(c4_gold):
     np.testing.assert_array_equal(np.stack(preds), g["tokens"])
     assert model.stats["passes"] == int(g["passes"].max())
     np.testing.assert_array_equal(model.stats["row_passes"], g["passes"])
-    if name == "large_v3_ts_mp_b32_fp32":
-        assert int((g["passes"] >= 2).sum()) >= 8
-        print(f"\nconfig4 multi-pass fixture: seek passes per row {g['passes'].tolist()}; fp32 engine bit-exact")
     del model
     _free()
 
@@ -610,6 +607,82 @@ def test_config4_bf16_pseudo_label_w1_w2(c4_gold, tmp_path):
     print("config4 bf16 pseudo_label: W=2 (gloo, 2 processes on cuda:0, batch 16 each) == W=1 on 32 items")
 
 
+def _teacher_forced_per_pass(model, feats, g, floor=MARGIN_FLOOR):
+    """The bf16 engine teacher-forced along EVERY seek pass of transformers' fp32 run (the fixture's PassRecorder
+    arrays): each pass's segment input is rebuilt from ``feats`` at the recorded seek / frame count (zero-padded to
+    3000 frames, generation_whisper.py:1831-1850), encoded by the bf16 engine, and the fp32 pass's sequence is fed
+    through the production decode kernels; the processed greedy choice (Suppress -> SuppressAtBegin ->
+    WhisperTimeStamp, logits_process.py:1816-2047, applied by the oracle to the engine's logits) must equal the fp32
+    token at every step whose fp32 margin is >= ``floor``.  Returns (compared, total, compared in passes >= 2,
+    total in passes >= 2, differing (pass entry, step) pairs)."""
+    from oracle.generate import process_logits
+
+    gen = generation_constants(LARGE_V3)
+    gd = gen.to_dict()
+    eng, P = model.engine, 3
+    n_cmp = n_tot = n_cmp2 = n_tot2 = 0
+    bad = []
+    for it in np.unique(g["pass_iter"]):
+        ks = np.nonzero(g["pass_iter"] == it)[0]
+        seg = torch.zeros((len(ks), feats.shape[1], 3000), device="cuda")
+        for i, k in enumerate(ks):
+            r, s0, nf = int(g["pass_row"][k]), int(g["pass_seek"][k]), int(g["pass_nframes"][k])
+            seg[i, :, :nf] = feats[r, :, s0: s0 + nf]
+        L = int(P + g["pass_len"][ks].max())
+        seq = g["pass_seq"][ks][:, :L].copy()
+        seq[seq < 0] = gen.eos_token_id  # beyond a row's end: any id (causal, never read back)
+        sess = eng.new_session(len(ks), eng.encode(seg))
+        lg = sess.teacher_forced_logits(torch.from_numpy(seq[:, :-1]), P)
+        for i, k in enumerate(ks):
+            n = int(g["pass_len"][k])
+            rows = lg[i, :n].float().cpu().numpy()
+            safe = g["pass_margin"][k, :n] >= floor
+            for t in np.nonzero(safe)[0]:
+                proc = process_logits(seq[i: i + 1, : P + t], rows[t: t + 1], gd, P, True)
+                if int(proc.argmax()) != int(seq[i, P + t]):
+                    bad.append((int(k), int(t)))
+            n_cmp += int(safe.sum())
+            n_tot += n
+            if it >= 1:
+                n_cmp2 += int(safe.sum())
+                n_tot2 += n
+        del sess, lg
+    return n_cmp, n_tot, n_cmp2, n_tot2, bad
+
+
+def test_config4_hipmel_multipass(gold):
+    """Config 4's multi-pass case on the PRODUCT's own inputs: tests/golden/large_v3_c4_hipmel.npz
+    holds the HIP log-mel that kwhisper.WhisperFeatureExtractor gave stand-in clips 1 and 522 (and six one-pass clips)
+    on the GPU box (tools/dump_hipmel.py), and transformers' fp32 / bf16 large-v3 run on exactly those features
+    (tools/make_fixtures.py --only c4_hipmel; run_pseudo_labelling.py:99-102,268,338).  The fp32 engine, through
+    pseudo_label(), is bit-exact with transformers' fp32 tokens and per-row seek passes; the bf16 engine is
+    teacher-forced along every fp32 pass and its safe-margin greedy choice must equal the fp32 token."""
+    g = gold("large_v3_c4_hipmel")
+    feats = torch.from_numpy(g["features"]).cuda()
+    n = feats.shape[0]
+    m32 = _model(LARGE_V3, torch.float32)
+    ids, preds = _c4_pseudo_label(m32, g["durations"], feats, n)
+    assert ids == list(range(n))
+    np.testing.assert_array_equal(np.stack(preds), g["tokens"])
+    np.testing.assert_array_equal(m32.stats["row_passes"], g["passes"])
+    print(f"\nconfig4 HIP log-mel fixture (clips {g['clip_ids'].tolist()}): transformers fp32 seek passes "
+          f"{g['passes'].tolist()} (bf16 reference {g['bf16_passes'].tolist() if 'bf16_passes' in g else '-'}); fp32 "
+          f"engine bit-exact, same passes")
+    del m32
+    _free()
+    m16 = _model(LARGE_V3, torch.bfloat16)
+    n_cmp, n_tot, n_cmp2, n_tot2, bad = _teacher_forced_per_pass(m16, feats, g)
+    t16 = m16.generate(feats, **C4_KW).cpu().numpy()
+    print(f"config4 HIP log-mel bf16 teacher-forced per pass: {n_cmp} of {n_tot} steps compared (margin >= "
+          f"{MARGIN_FLOOR}; passes >= 2: {n_cmp2} of {n_tot2}), {len(bad)} differ; free-running bf16 passes "
+          f"{m16.stats['row_passes'].tolist()}, rows identical to fp32 "
+          f"{sum(np.array_equal(a, b) for a, b in zip(t16, g['tokens']))}/{n}")
+    assert len(bad) == 0, f"(pass entry, step) pairs whose safe-margin greedy choice differs: {bad[:8]}"
+    assert n_cmp2 > 0 and n_cmp >= 0.9 * n_tot
+    del m16
+    _free()
+
+
 @pytest.mark.parametrize("fixture", ["large_v3_longform_fp32", "large_v3_longform8_fp32"])
 def test_large_v3_longform_multipass(gold, fixture):
     """The seek loop's second and later passes at large-v3.  No config-4 stand-in clip takes a
@@ -636,10 +709,61 @@ def test_large_v3_longform_multipass(gold, fixture):
     t16 = m16.generate(feats, attention_mask=mask, **kw).cpu().numpy()
     w = min(t16.shape[1], g["tokens"].shape[1])
     n = _gated_equal(t16[:, :w], g["tokens"][:, :w], g["margin"][:, :w])
-    print(f"\n{fixture}: passes per row {g['passes'].tolist()} (fp32 engine bit-exact, same passes); bf16 "
-          f"{n} of {g['tokens'].size} tokens compared (margin >= {MARGIN_FLOOR}), all equal; bf16 passes "
-          f"{m16.stats['row_passes'].tolist()}")
+    print(f"\n{fixture}: passes per row {g['passes'].tolist()} (fp32 engine bit-exact, same passes); bf16 free-running "
+          f"{n} of {g['tokens'].size} tokens compared (margin >= {MARGIN_FLOOR}, up to each row's first unsafe step), "
+          f"all equal; bf16 passes {m16.stats['row_passes'].tolist()}")
+    # every pass, teacher-forced (the free-running gate stops each row at its first low margin)
+    n_cmp, n_tot, n_cmp2, n_tot2, bad = _teacher_forced_per_pass(m16, feats, g)
+    print(f"{fixture}: bf16 teacher-forced per pass: {n_cmp} of {n_tot} steps compared (passes >= 2: {n_cmp2} of "
+          f"{n_tot2}), {len(bad)} differ")
+    assert len(bad) == 0, f"(pass entry, step) pairs whose safe-margin greedy choice differs: {bad[:8]}"
+    assert n_cmp2 > 0 and n_cmp >= 0.9 * n_tot
     del m16
+    _free()
+
+
+def test_lanes_cold_capture_multipass(gold):
+    """lanes that start COLD -- no warm-up batch, so every session allocation and hipGraph capture
+    (prefill, one step, K steps, for every batch size the seek loop shrinks to) happens on the lane threads while the
+    other lane is running -- return exactly the one-lane results.  Two model.lane() handles decode the two halves of
+    the eight-clip multi-pass long-form batch (passes 2-3 per row, batch 4 -> 3 -> ... rows) at the same time from
+    two host threads, each on its own stream; captures are serialised by decode.CAPTURE_LOCK."""
+    import threading
+
+    from _util import longform_inputs
+
+    g = gold("large_v3_longform8_fp32")
+    feats, mask, _ = longform_inputs(g["clips"], n_mels=LARGE_V3.num_mel_bins)
+    feats, mask = torch.from_numpy(feats).cuda(), torch.from_numpy(mask).cuda()
+    kw = dict(language="ja", task="transcribe", return_timestamps=True, max_length=int(g["max_length"]))
+    m16 = _model(LARGE_V3, torch.bfloat16)
+    halves = [slice(0, 4), slice(4, 8)]
+    lanes = [m16.lane(), m16.lane()]  # before any generate: nothing captured anywhere yet
+    got, errs = [None, None], []
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    start = threading.Barrier(2)
+
+    def run(i):
+        try:
+            with torch.cuda.stream(streams[i]):
+                start.wait()
+                got[i] = lanes[i].generate(feats[halves[i]], attention_mask=mask[halves[i]], **kw).cpu().numpy()
+        except BaseException as e:
+            errs.append(e)
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    torch.cuda.synchronize()
+    for i, h in enumerate(halves):  # the one-lane reference (the caller's own handle, captured afterwards)
+        want = m16.generate(feats[h], attention_mask=mask[h], **kw).cpu().numpy()
+        np.testing.assert_array_equal(got[i], want, err_msg=f"lane {i}")
+    print(f"\ncold lanes: two lanes captured their graphs concurrently (passes "
+          f"{[lanes[i].stats['row_passes'].tolist() for i in range(2)]}); outputs equal the one-lane runs")
+    del m16, lanes
     _free()
 
 

@@ -350,46 +350,104 @@ def large_config4_fixtures():
     print(f"large_v3_ts_b32 fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
 
 
-def large_config4_multipass_fixtures(ids_json):
-    """tests/golden/large_v3_ts_mp_b32_fp32.npz: config 4 at its own teacher on a 32-clip batch in which at least
-    8 clips take a SECOND seek pass (the first 32 stand-in clips all finish in one).  The clip
-    ids come from ``ids_json`` (tools/find_multipass.py's output over the fp32 engine, bit-exact with transformers):
-    the first 16 multi-pass clips plus the first 16 single-pass ones, in id order.  transformers' fp32 large-v3 then
-    decodes that batch with the reference's settings (run_pseudo_labelling.py:99-102,338; max_length 128, the
-    cumulative growth generation_whisper.py:1935-1940): tokens, per-token margins through the seek passes, passes
-    per row, segments."""
-    t0 = time.time()
-    with open(ids_json) as f:
-        found = json.load(f)
-    passes_found = np.asarray(found["passes"])
-    multi = [int(i) for i in np.nonzero(passes_found >= 2)[0][:16]]
-    single = [int(i) for i in np.nonzero(passes_found == 1)[0][:32 - len(multi)]]
-    ids = sorted(multi + single)
-    assert len(ids) == 32 and len(multi) >= 8, (len(ids), len(multi))
-    durs_all = S.reazon_durations()
-    durs = durs_all[ids]
-    audio = [S.reazon_audio(i, float(durs_all[i])) for i in ids]
-    fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins)
-    feats = torch.from_numpy(fe(audio, sampling_rate=16000, return_tensors="np")["input_features"])
-    m = hf_model(LARGE_V3)
-    m.generation_config, gc = hf_gen_config(LARGE_V3)
-    kw = dict(language="ja", task="transcribe", return_timestamps=True, max_length=128)
-    res = run_generate(m, feats, return_dict_in_generate=True, output_scores=True, **kw)
-    print(f"  large_v3_ts_mp_b32: generate ({time.time() - t0:.1f}s)")
+class PassRecorder:
+    """Records every iteration of transformers' seek loop (generation_whisper.py:785-903) on one model: which rows
+    ran (batch_idx_map), each row's ``seek`` and ``seek_num_frames`` as ``_get_input_segment`` (:1831-1850) received
+    them, and the per-row generate output of the pass (``generate_with_fallback``'s seek_outputs: the sequence with
+    its prompt and the processed per-step scores).  Instance attributes shadow the two methods for one run."""
+
+    def __init__(self, m):
+        self.m, self.iters = m, []
+        seg, gwf = type(m)._get_input_segment, m.generate_with_fallback
+
+        def get_input_segment(input_features, seek, seek_num_frames, num_segment_frames, cur_bsz, batch_idx_map):
+            rows = [int(batch_idx_map[i]) for i in range(cur_bsz)]
+            self.iters.append({"rows": rows, "seek": [int(seek[r]) for r in rows],
+                               "nframes": [int(seek_num_frames[r]) for r in rows]})
+            return seg(input_features, seek, seek_num_frames, num_segment_frames, cur_bsz, batch_idx_map)
+
+        def generate_with_fallback(**kw):
+            out = gwf(**kw)
+            self.iters[-1]["outputs"] = out[1]
+            return out
+
+        m._get_input_segment, m.generate_with_fallback = get_input_segment, generate_with_fallback
+
+    def close(self):
+        del self.m._get_input_segment, self.m.generate_with_fallback
+
+    def arrays(self, P: int) -> dict:
+        """One entry per (seek iteration, active row): pass_iter, pass_row, pass_seek, pass_nframes, pass_len
+        (generated steps incl. a final EOS), pass_seq (prompt + generated, -1 padded) and pass_margin (top-1 - top-2
+        of the processed scores at each step, +inf padded)."""
+        ent = []
+        for it, rec in enumerate(self.iters):
+            for i, r in enumerate(rec["rows"]):
+                o = rec["outputs"][i]
+                sc = torch.stack(list(o["scores"]), 0).float()
+                seq = o["sequences"].reshape(-1)[: P + sc.shape[0]]
+                assert torch.equal(sc.argmax(-1), seq[P:]), "greedy step != argmax of its scores"
+                top = sc.topk(2, -1).values
+                ent.append((it, r, rec["seek"][i], rec["nframes"][i], seq.numpy(), (top[:, 0] - top[:, 1]).numpy()))
+        T = max(len(e[4]) for e in ent)
+        seqs = np.full((len(ent), T), -1, np.int64)
+        marg = np.full((len(ent), T - P), np.inf, np.float32)
+        for k, e in enumerate(ent):
+            seqs[k, : len(e[4])] = e[4]
+            marg[k, : len(e[5])] = e[5]
+        return {"pass_iter": np.array([e[0] for e in ent], np.int64), "pass_row": np.array([e[1] for e in ent], np.int64),
+                "pass_seek": np.array([e[2] for e in ent], np.int64),
+                "pass_nframes": np.array([e[3] for e in ent], np.int64),
+                "pass_len": np.array([len(e[5]) for e in ent], np.int64), "pass_seq": seqs, "pass_margin": marg}
+
+
+def _c4_outputs(res, n_rows, P, gc):
     toks = res["sequences"].numpy().astype(np.int64)
-    P = 3
     margin = np.full(toks.shape, np.inf, np.float32)
-    passes = np.zeros(len(audio), np.int64)
+    passes = np.zeros(n_rows, np.int64)
     for b, segs in enumerate(res["segments"]):
         mg, tk, passes[b] = _aligned_margins(segs, P)
         assert np.array_equal(tk, toks[b, : len(tk)]) and (toks[b, len(tk):] == gc.pad_token_id).all()
         margin[b, : len(mg)] = mg
     segs = [[(float(x["start"]), float(x["end"]), len(x["tokens"])) for x in row] for row in res["segments"]]
-    out = {"clip_ids": np.asarray(ids, np.int64), "durations": durs.astype(np.float64), "tokens": toks,
-           "margin": margin, "passes": passes, "engine_passes": passes_found[ids].astype(np.int64),
-           "segments": np.array(json.dumps(segs)), "max_length": 128}
-    np.savez_compressed(os.path.join(GOLD, "large_v3_ts_mp_b32_fp32.npz"), **out)
-    print(f"large_v3_ts_mp_b32 fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
+    return toks, margin, passes, segs
+
+
+def large_config4_hipmel_fixtures(features_npz, bf16=True):
+    """tests/golden/large_v3_c4_hipmel.npz: config 4's multi-pass case on the PRODUCT's own inputs (VERDICT r4 item
+    1).  ``features_npz`` is tools/dump_hipmel.py's output from the GPU box: the exact f32 log-mel that the HIP feature
+    extractor gives stand-in clips 1 and 522 (three seek passes in the fp32 engine, profiles/r04c_multipass_find.json)
+    and six single-pass clips.  transformers' fp32 large-v3 decodes exactly those features with the reference's
+    settings (run_pseudo_labelling.py:99-102,268,338; max_length 128 with the cumulative growth
+    generation_whisper.py:1935-1940): tokens, per-token margins, seek passes per row, segments, and every pass's
+    sequence / seek / margins (PassRecorder).  With ``bf16`` the same HF model cast to bfloat16 (the reference's own
+    teacher precision, :229,338) also decodes them: its tokens and passes."""
+    t0 = time.time()
+    z = np.load(features_npz)
+    feats = torch.from_numpy(z["features"].astype(np.float32))
+    m = hf_model(LARGE_V3)
+    m.generation_config, gc = hf_gen_config(LARGE_V3)
+    kw = dict(language="ja", task="transcribe", return_timestamps=True, max_length=128)
+    rec = PassRecorder(m)
+    res = run_generate(m, feats, return_dict_in_generate=True, output_scores=True, **kw)
+    rec.close()
+    P = 3
+    toks, margin, passes, segs = _c4_outputs(res, feats.shape[0], P, gc)
+    print(f"  large_v3_c4_hipmel: fp32 generate ({time.time() - t0:.1f}s), passes {passes.tolist()}")
+    out = {"clip_ids": z["clip_ids"], "durations": z["durations"], "features": z["features"].astype(np.float32),
+           "tokens": toks, "margin": margin, "passes": passes, "segments": np.array(json.dumps(segs)),
+           "max_length": 128, **rec.arrays(P)}
+    if bf16:
+        m.generation_config, _ = hf_gen_config(LARGE_V3)
+        m = m.to(torch.bfloat16)
+        r16 = PassRecorder(m)
+        t16 = run_generate(m, feats.to(torch.bfloat16), return_segments=True, **kw)
+        r16.close()
+        out["bf16_tokens"] = t16["sequences"].numpy().astype(np.int64)
+        out["bf16_passes"] = np.bincount([r for it in r16.iters for r in it["rows"]], minlength=feats.shape[0])
+        print(f"  large_v3_c4_hipmel: bf16 generate ({time.time() - t0:.1f}s), passes {out['bf16_passes'].tolist()}")
+    np.savez_compressed(os.path.join(GOLD, "large_v3_c4_hipmel.npz"), **out)
+    print(f"large_v3_c4_hipmel fixtures done in {time.time() - t0:.1f}s {toks.shape}")
 
 
 LARGE_LONG_CLIPS = [("tone", 0, 45.0), ("dummy", 3, 70.0)]
@@ -414,21 +472,16 @@ def large_longform_fixtures(name="large_v3_longform_fp32", clips=None):
     inp = fe(audio, sampling_rate=16000, return_tensors="pt", truncation=False, padding="longest",
              return_attention_mask=True)
     m.generation_config, gc = hf_gen_config(LARGE_V3)
+    rec = PassRecorder(m)  # r05: every pass's sequence / seek / margins, for the bf16 per-pass teacher-forced check
     res = run_generate(m, inp["input_features"], attention_mask=inp["attention_mask"], return_timestamps=True,
                        language="ja", task="transcribe", max_length=128, return_dict_in_generate=True,
                        output_scores=True)
+    rec.close()
     print(f"  large_v3_longform: generate ({time.time() - t0:.1f}s)")
-    toks = res["sequences"].numpy().astype(np.int64)
     P = 3
-    margin = np.full(toks.shape, np.inf, np.float32)
-    passes = np.zeros(len(audio), np.int64)
-    for b, segs in enumerate(res["segments"]):
-        mg, tk, passes[b] = _aligned_margins(segs, P)
-        assert np.array_equal(tk, toks[b, : len(tk)]) and (toks[b, len(tk):] == gc.pad_token_id).all()
-        margin[b, : len(mg)] = mg
-    segs = [[(float(x["start"]), float(x["end"]), len(x["tokens"])) for x in row] for row in res["segments"]]
+    toks, margin, passes, segs = _c4_outputs(res, len(audio), P, gc)
     out = {"clips": np.array([f"{k}:{s}:{sec}" for k, s, sec in clips]), "tokens": toks, "margin": margin,
-           "passes": passes, "segments": np.array(json.dumps(segs)), "max_length": 128}
+           "passes": passes, "segments": np.array(json.dumps(segs)), "max_length": 128, **rec.arrays(P)}
     np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), **out)
     print(f"{name} fixtures done in {time.time() - t0:.1f}s {toks.shape}, passes {passes.tolist()}")
 
@@ -565,8 +618,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-large", action="store_true")
     ap.add_argument("--only", default=None)
-    ap.add_argument("--multipass-ids", default="profiles/r04_multipass_clips.json",
-                    help="--only large_c4_mp: tools/find_multipass.py output naming the multi-pass clips")
+    ap.add_argument("--hipmel", default="gpurun_out/c4_hipmel_features.npz",
+                    help="--only c4_hipmel: tools/dump_hipmel.py output (the box's HIP log-mel of the chosen clips)")
+    ap.add_argument("--no-bf16", action="store_true", help="--only c4_hipmel: skip the bf16 reference run")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     torch.manual_seed(0)
@@ -607,8 +661,8 @@ def main():
         large_longform_fixtures()
     if not a.skip_large and a.only == "large_longform8":
         large_longform_fixtures("large_v3_longform8_fp32", LARGE_LONG8_CLIPS)
-    if not a.skip_large and a.only == "large_c4_mp":
-        large_config4_multipass_fixtures(a.multipass_ids)
+    if not a.skip_large and a.only == "c4_hipmel":
+        large_config4_hipmel_fixtures(a.hipmel, bf16=not a.no_bf16)
     if not a.skip_large and a.only in (None, "kotoba_beam"):
         kotoba_beam_fixtures()
     if a.only in (None, "pipeline"):
