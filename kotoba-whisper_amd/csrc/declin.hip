@@ -72,19 +72,27 @@ struct DecP {
   int zrows; // rows per grid z-chunk: 32, or 16 for narrow grids (row split, launch())
 };
 
-// The fused MLP's fc1 hand-off (dec_mlp_kernel below): instead of storing its bf16 GELU tile to C, a PUB
-// workgroup (NCB = 2: its 32 columns are k-tile cg of fc2's K) writes the tile to hx in the MFMA A-fragment
-// layout fc2's waves load ([k-tile][row half][64 lanes][16 B]) by 16-B sc1 (write-through) stores, drains them and
-// sets flags[cg] (MI355X_MICROARCH visibility table, first row: sc1 stores, one lane's agent-scope flag, sc1 loads).
+// The fused MLP's hand-off (dec_mlp_kernel below).  Producer (PUB, fc1): instead of storing its bf16 GELU tile to
+// C, a workgroup writes the tile to hx in the MFMA A-fragment layout fc2's waves load ([k-tile][row half][64 lanes]
+// [16 B]) by 16-B sc1 (write-through) stores, drains them and sets flags[cg] (MI355X_MICROARCH visibility table,
+// first row: sc1 stores, one lane's agent-scope flag, sc1 loads).  Consumer (CONS, fc2): a wave polls the flags of
+// its own k-tiles (two 16-column producers per k-tile), then loads their fragments by sc1 loads; the last consumer
+// workgroup through (done counter) re-arms the flags for the next launch.
 struct MlpPub {
   char* hx;
   int* flags;
-  int* fault;  // test hook: nonzero -> workgroup 0 skips its flag once (kw_dec_mlp_status_offset)
+  int* fault;   // test hook: nonzero -> workgroup 0 skips its flag once (kw_dec_mlp_status_offset)
+  int* status;  // consumer: a poll timed out (its rows are NaN)
+  int* done;    // consumer workgroups past their polls
+  int n_cons, n_flags;
 };
 
 // H2: the second 16-row half of the tile exists (false: a row-split chunk of <= 16 rows -- its a1 / c1 / LayerNorm
 // statistics are never loaded or computed, which frees the registers for two workgroups per CU)
-template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool PUB, bool H2 = true>
+// (mlp_wait: the consumer's flag poll, defined with the fused MLP below)
+__device__ __forceinline__ bool mlp_wait(const int* flags, int fidx, int lane, int* status);
+
+template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool PUB, bool H2 = true, bool CONS = false>
 __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int cg, const int ks, const int nw,
                                                 const MlpPub& pub) {
   __shared__ f32x4 red[MAXW][NCB][2][64];
@@ -114,7 +122,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
       w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)(cg * NCB + c) * nkt + min(kt0 + u, ktl)) * 64 + lane);
   const int wkt0 = (nkt * ks) / ksn, wkt1 = (nkt * (ks + 1)) / ksn;  // this workgroup's k-tiles
   const int cpr = (wkt1 - wkt0) * 4, cprp = cpr + 1;
-  const bool xlds = p.xlds;
+  const bool xlds = !CONS && p.xlds;
   if (xlds) {
     // <= 16 rows: only the pieces of rows 0..15 (the second row half's fragments then hold stale LDS, and its
     // output rows -- all >= M -- are discarded; every row of an MFMA tile is independent of the others)
@@ -158,7 +166,31 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     }
   }
 
-  if (xlds) {
+  if constexpr (CONS) {
+    // the producers' fragments of this wave's k-tiles: one poll over their flags (lane l: flag 2 kt0 + l), then sc1
+    // loads (written in this launch by other CUs); a poll that timed out turns the operands into NaN
+    const int fidx = lane < 2 * (kt1 - kt0) ? 2 * kt0 + lane : -1;
+    const bool ok = mlp_wait(pub.flags, fidx, lane, pub.status);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx, (short)0, nkt * 2048, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < KTM; ++u) {
+      const int kt = min(kt0 + u, ktl);
+      a0[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 0) * 1024 + lane * 16, 0, 16));
+      if constexpr (H2)
+        a1[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 1) * 1024 + lane * 16, 0, 16));
+    }
+    if (!ok) {
+      bf16x8 nan;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nan[e] = (__bf16)__builtin_nanf("");
+#pragma unroll
+      for (int u = 0; u < KTM; ++u) {
+        a0[u] = nan;
+        a1[u] = nan;
+      }
+    }
+  } else if (xlds) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #pragma unroll
@@ -238,6 +270,14 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     }
     __syncthreads();
     if (wave != 0) return;
+    if constexpr (CONS) {  // every wave of this workgroup is past its polls: the last consumer re-arms the flags
+      int last = 0;
+      if (lane == 0) last = __hip_atomic_fetch_add(pub.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pub.n_cons - 1;
+      if (__shfl(last, 0, 64)) {
+        for (int i = lane; i < pub.n_flags; i += 64) __hip_atomic_store(pub.flags + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0) __hip_atomic_store(pub.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     for (int w2 = 1; w2 < nw; ++w2)
 #pragma unroll
       for (int c = 0; c < NCB; ++c) {
@@ -333,8 +373,8 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
           if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
           if (n < p.scale_cols) v *= p.scale;
           if constexpr (PUB) {
-            // every row (rows >= M are clamped copies: fc2 discards them), row-major 32 x 32 tile in LDS
-            reinterpret_cast<bf16_t*>(xs)[m * 40 + c * 16 + (lane & 15)] = f2bf(v);
+            // every row (rows >= M are clamped copies: fc2 discards them), row-major 32 x 16 NCB tile in LDS
+            reinterpret_cast<bf16_t*>(xs)[m * (16 * NCB + 8) + c * 16 + (lane & 15)] = f2bf(v);
           } else {
             if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
           }
@@ -348,12 +388,19 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx + (int64_t)cg * 2048, (short)0, 2048, 0x00020000);
+    if constexpr (NCB == 2) {  // 32 columns = fc2's k-tile cg
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx + (int64_t)cg * 2048, (short)0, 2048, 0x00020000);
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const u32x4 t = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(xs) + (16 * hh + (lane & 15)) * 40 +
-                                                      8 * (lane >> 4));
-      __builtin_amdgcn_raw_buffer_store_b128(t, rs, (hh * 64 + lane) * 16, 0, 16);  // aux 16 = sc1
+      for (int hh = 0; hh < 2; ++hh) {
+        const u32x4 t = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(xs) + (16 * hh + (lane & 15)) * 40 +
+                                                        8 * (lane >> 4));
+        __builtin_amdgcn_raw_buffer_store_b128(t, rs, (hh * 64 + lane) * 16, 0, 16);  // aux 16 = sc1
+      }
+    } else {  // 16 columns = half q = cg & 1 of k-tile cg >> 1: fragment lanes r + 16 (2 q + j), one 16-B piece per lane
+      const int hh = lane >> 5, r = lane & 15, j = (lane >> 4) & 1;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx + (int64_t)(cg >> 1) * 2048, (short)0, 2048, 0x00020000);
+      const u32x4 t = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(xs) + (16 * hh + r) * 24 + 8 * j);
+      __builtin_amdgcn_raw_buffer_store_b128(t, rs, (hh * 64 + r + 16 * (2 * (cg & 1) + j)) * 16, 0, 16);
     }
     const int fault = __hip_atomic_load(pub.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -391,28 +438,27 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
 }
 
 // ---- fused decode MLP: fc1 (LayerNorm-fused, GELU) -> fc2 (+ residual) in ONE launch (kw_dec_mlp) ----
-// Workgroups [0, n1): fc1 exactly as dec_linear_kernel<5, 2, true, STORE, bf16> computes it (dec_linear_body), each
-// publishing its 32 columns -- one k-tile of fc2's K -- through MlpPub.  Workgroups [n1, n1 + N/16): one per 16
-// columns of fc2, each doing ALL of that column block's work of the two-launch plan's split-K fc2 (ks K-splits x nw2
-// waves = ks * nw2 slices of <= 5 k-tiles, spread over its 8 waves): every slice's weight fragments are in flight from
-// the start (they stream while fc1 runs: the split-K launch's weight round trip and the launch boundary leave the
-// chain), a slice waits only for the flags of its own k-tiles, loads their fragments by sc1 loads, and its MFMA
-// partial goes to LDS; wave 0 then sums the partials in the two-launch plan's order (waves of a K-split, then the
-// K-splits with the seam's zero terms) and applies the RESID epilogue -- h and hb bitwise those of the two
-// launches.  Every wait is on a workgroup dispatched earlier in the same launch (fc1 never waits), so the launch
-// cannot deadlock at any residency; the last fc2 workgroup through re-arms the flags.  A poll that outlasts
-// MLP_SPIN_LIMIT sets the status word and writes NaN rows (kw_dec_mlp_status_offset).
-constexpr int MLP_SLW = 5;               // fc2 slices per wave (<= 8 x 5 = 40 slices)
+// r05, co-resident roles: workgroups [0, n1) are fc1, one per 16 columns (dec_linear_body<5, 1,
+// LN, STORE, GELU>: 8 waves x 5 k-tiles, each activation fragment loaded straight from hb -- no LDS image, so the
+// launch needs no more LDS than its reduction buffers), each publishing its tile -- half of one of fc2's k-tiles --
+// through MlpPub; workgroups [n1, n1 + n2) are fc2's split-K grid (one per (16 columns, K-split): 8 waves x 5 k-tiles,
+// the deterministic seam of the split-K launch), every one of them spread over the CUs beside fc1 and streaming its
+// weights while fc1 runs; a wave waits only for the flags of its own k-tiles.  r04's version gave fc2 80 workgroups
+// of all the K-splits each: it read the whole activation per workgroup and lost (19.8 vs 18.6 us).  Every wait is on
+// a workgroup dispatched earlier in the same launch (fc1 never waits), so the launch cannot deadlock at any
+// residency; a poll that outlasts MLP_SPIN_LIMIT sets the status word and writes NaN rows
+// (kw_dec_mlp_status_offset).  fc1's values are bitwise those of its own launch (the same per-element arithmetic);
+// fc2 sums its K in 5-k-tile slices, 4 K-splits (f32 summation order of its own).
 constexpr int MLP_HDR = 1024;            // workspace ints before the fragment image: flags, done, status, fault
 constexpr int MLP_DONE = MLP_HDR - 4, MLP_STATUS = MLP_HDR - 3, MLP_FAULT = MLP_HDR - 2;
 constexpr int MLP_SPIN_LIMIT = 1 << 22;
+constexpr int MLP_CNT = 1024;            // fc2 seam counters (one per column block)
 
 struct MlpArgs {
-  DecP f1, f2;  // fc1: LayerNorm-fused STORE (gelu, bf16, xlds); fc2: RESID (h, hb)
-  char* hx;     // fc1's output as fc2 A-fragments: [F / 32][2][64][16 B]
-  int* ws;      // MLP_HDR ints: flags[F / 32], done, status, fault
-  int n1;       // fc1 workgroups (= F / 32 k-tiles of fc2)
-  int ks2, nw2; // fc2's two-launch geometry (choose(d, F))
+  DecP f1, f2;  // fc1: LayerNorm-fused STORE (gelu, bf16, no LDS image); fc2: RESID (h, hb), split-K seam
+  MlpPub pub;
+  int n1;       // fc1 workgroups (= F / 16)
+  int ncb2, ks2;  // fc2 column blocks and K-splits (n2 = ncb2 * ks2 workgroups)
 };
 
 // One wave polls up to 64 flags at once: lane l the flag fidx (< 0: none).
@@ -430,149 +476,12 @@ __device__ __forceinline__ bool mlp_wait(const int* flags, int fidx, int lane, i
   }
 }
 
-__device__ __forceinline__ void mlp_fc2_role(const MlpArgs& a, const int cb) {
-  extern __shared__ __attribute__((aligned(16))) char xs[];
-  __shared__ int tmo[MAXW];  // per wave: a poll of this wave timed out
-  f32x4(*part)[2][64] = reinterpret_cast<f32x4(*)[2][64]>(xs);  // [slice][row half][lane]
-  const DecP& p = a.f2;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nkt = p.K >> 5, ksn = a.ks2, nw2 = a.nw2, S = ksn * nw2;
-  const int M = p.M;
-  // 1. every slice's weights in flight (non-temporal), then the epilogue operands (wave 0)
-  bf16x8 w[MLP_SLW][5];
-#pragma unroll
-  for (int j = 0; j < MLP_SLW; ++j) {
-    const int sl = wave + 8 * j;
-    if (sl < S) {
-      const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S, ktl = max(kt1 - 1, kt0);
-#pragma unroll
-      for (int u = 0; u < 5; ++u)
-        w[j][u] = __builtin_nontemporal_load(p.W + ((int64_t)cb * nkt + min(kt0 + u, ktl)) * 64 + lane);
-    }
-  }
-  const int n_e = min(cb * 16 + (lane & 15), p.N - 1);
-  float hold[2][4], ebias = 0.f;
-  if (wave == 0) {
-    ebias = p.bias ? p.bias[n_e] : 0.f;
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) hold[hh][r] = p.h[(int64_t)min(16 * hh + 4 * (lane >> 4) + r, M - 1) * p.ldh + n_e];
-  }
-  // 2. ONE poll for the flags of every k-tile of this wave's slices (fc1's workgroups finish together: a poll per
-  //    slice paid a round trip each, r04i), then the slices' A fragments (sc1: written in this launch by other CUs)
-  //    double-buffered, slice j + 1's loads in flight under slice j's MFMAs; partials -> LDS
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.hx, (short)0, nkt * 2048, 0x00020000);
-  int fidx = -1;
-  {
-    int cum = 0;
-#pragma unroll
-    for (int j = 0; j < MLP_SLW; ++j) {
-      const int sl = wave + 8 * j;
-      if (sl < S) {
-        const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S;
-        if (lane >= cum && lane < cum + (kt1 - kt0)) fidx = kt0 + lane - cum;
-        cum += kt1 - kt0;
-      }
-    }
-  }
-  const bool ok = mlp_wait(a.ws, fidx, lane, a.ws + MLP_STATUS);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
-  bf16x8 av[2][2][5];  // [buffer][row half][k-tile]
-  auto load = [&](int j, int buf) {
-    const int sl = wave + 8 * j;
-    const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S, ktl = max(kt1 - 1, kt0);
-#pragma unroll
-    for (int u = 0; u < 5; ++u) {
-      const int kt = min(kt0 + u, ktl);
-      av[buf][0][u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 0) * 1024 + lane * 16, 0, 16));
-      av[buf][1][u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 1) * 1024 + lane * 16, 0, 16));
-    }
-  };
-  if (wave < S) load(0, 0);
-#pragma unroll
-  for (int j = 0; j < MLP_SLW; ++j) {
-    const int sl = wave + 8 * j;
-    if (sl >= S) break;
-    if (sl + 8 < S) load(j + 1, (j + 1) & 1);
-    const int kt0 = (nkt * sl) / S, kt1 = (nkt * (sl + 1)) / S;
-    f32x4 c0 = f32x4{0.f, 0.f, 0.f, 0.f}, c1 = c0;
-#pragma unroll
-    for (int u = 0; u < 5; ++u)
-      if (kt0 + u < kt1) {
-        c0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[j & 1][0][u], w[j][u], c0, 0, 0, 0);
-        c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[j & 1][1][u], w[j][u], c1, 0, 0, 0);
-      }
-    part[sl][0][lane] = c0;
-    part[sl][1][lane] = c1;
-  }
-  if (lane == 0) tmo[wave] = ok ? 0 : 1;
-  __syncthreads();
-  if (wave != 0) return;
-  // every wave of this workgroup is past its polls: the last fc2 workgroup through re-arms the flags
-  int last = 0;
-  if (lane == 0) last = __hip_atomic_fetch_add(a.ws + MLP_DONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
-                        (int)gridDim.x - a.n1 - 1;
-  if (__shfl(last, 0, 64)) {
-    for (int i = lane; i < nkt; i += 64) __hip_atomic_store(a.ws + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lane == 0) __hip_atomic_store(a.ws + MLP_DONE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // 3. the two-launch plan's sums: a K-split's waves in order (dec_linear_body step 4), then the seam's K-splits in
-  //    order with its zero terms up to KSMAX (step 5)
-  f32x4 c0, c1;
-  if (ksn == 1) {
-    c0 = part[0][0][lane];
-    c1 = part[0][1][lane];
-    for (int w2 = 1; w2 < nw2; ++w2) {
-      c0 += part[w2][0][lane];
-      c1 += part[w2][1][lane];
-    }
-  } else {
-    for (int q = 0; q < KSMAX; ++q) {
-      f32x4 s0 = f32x4{0.f, 0.f, 0.f, 0.f}, s1 = s0;
-      if (q < ksn) {
-        s0 = part[q * nw2][0][lane];
-        s1 = part[q * nw2][1][lane];
-        for (int w2 = 1; w2 < nw2; ++w2) {
-          s0 += part[q * nw2 + w2][0][lane];
-          s1 += part[q * nw2 + w2][1][lane];
-        }
-      }
-      if (q == 0) {
-        c0 = s0;
-        c1 = s1;
-      } else {
-        c0 += s0;
-        c1 += s1;
-      }
-    }
-  }
-  // 4. RESID epilogue (dec_linear_body step 6)
-  bool bad = false;
-  for (int w2 = 0; w2 < MAXW; ++w2) bad |= tmo[w2] != 0;
-  const int n = cb * 16 + (lane & 15);
-#pragma unroll
-  for (int hh = 0; hh < 2; ++hh)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = 16 * hh + 4 * (lane >> 4) + r;
-      float v = hh ? c1[r] : c0[r];
-      v += ebias;
-      v += hold[hh][r];
-      if (bad) v = __builtin_nanf("");
-      if (n < p.N && m < M) {
-        p.h[(int64_t)m * p.ldh + n] = v;
-        p.hb[(int64_t)m * p.ldh + n] = f2bf(v);
-      }
-    }
-}
-
 __global__ __launch_bounds__(512) void dec_mlp_kernel(MlpArgs a) {
   if ((int)blockIdx.x < a.n1) {
-    const MlpPub pub{a.hx, a.ws, a.ws + MLP_FAULT};
-    dec_linear_body<5, 2, true, KW_EPI_STORE, bf16_t, true>(a.f1, 1, blockIdx.x, 0, 8, pub);
+    dec_linear_body<5, 1, true, KW_EPI_STORE, bf16_t, true>(a.f1, 1, blockIdx.x, 0, 8, a.pub);
   } else {
-    mlp_fc2_role(a, blockIdx.x - a.n1);
+    const int j = blockIdx.x - a.n1;
+    dec_linear_body<5, 1, false, KW_EPI_RESID, float, false, true, true>(a.f2, a.ks2, j % a.ncb2, j / a.ncb2, 8, a.pub);
   }
 }
 
@@ -1379,31 +1288,31 @@ extern "C" int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed,
 // ---- kw_dec_mlp (dec_mlp_kernel): fc1 -> fc2 of a greedy decode step in one launch ----
 namespace {
 
-// The two-launch plan's geometries, and whether the fused kernel reproduces them: fc1 as 8 waves x 5 k-tiles with
-// 2 column blocks per workgroup (one k-tile of fc2 per workgroup), fc2 as K-split slices of <= 5 k-tiles that fit
-// 8 waves x MLP_SLW.
-bool mlp_geometry(int64_t M, int64_t d, int64_t F, Geo& g1, Geo& g2) {
+// fc1: 16-column workgroups of 8 waves x <= 5 k-tiles (K = d <= 1280); fc2: K-splits of 8 waves x 5 k-tiles
+// (ks2 = F / 1280 at large-v3), <= KSMAX splits
+bool mlp_geometry(int64_t M, int64_t d, int64_t F, int& ks2) {
   if (M < 1 || M > 32 || d <= 0 || F <= 0 || d % 32 != 0 || F % 32 != 0) return false;
-  g1 = choose(F, d);
-  g2 = choose(d, F);
   const int nkt1 = (int)(d / 32), nkt2 = (int)(F / 32);
-  if (g1.ncb != 2 || g1.ktm != 5 || g1.ks != 1 || g1.nw != 8 || (nkt1 + 7) / 8 > 5) return false;
-  if (g2.ncb != 1 || g2.ktm != 5 || g2.ks > KSMAX || g2.ks * g2.nw > 8 * MLP_SLW) return false;
-  if ((nkt2 + g2.ks * g2.nw - 1) / (g2.ks * g2.nw) > 5 || nkt2 > MLP_DONE) return false;
-  return true;
+  if (nkt1 > 8 * 5 || F / 16 > MLP_DONE || d / 16 > MLP_CNT) return false;
+  ks2 = (nkt2 + 39) / 40;
+  return ks2 <= KSMAX && (nkt2 + ks2 * 8 - 1) / (ks2 * 8) <= 5;
 }
+
+size_t mlp_hx_bytes(int64_t F) { return (size_t)(F / 32) * 2048; }
 
 }  // namespace
 
 extern "C" int kw_dec_mlp_supported(int64_t M, int64_t d, int64_t F) {
-  Geo g1, g2;
-  return mlp_geometry(M, d, F, g1, g2) ? 1 : 0;
+  int ks2;
+  return mlp_geometry(M, d, F, ks2) ? 1 : 0;
 }
 
 extern "C" size_t kw_dec_mlp_workspace(int64_t M, int64_t d, int64_t F) {
   (void)M;
-  (void)d;
-  return (size_t)MLP_HDR * sizeof(int) + (size_t)(F / 32) * 2048;
+  int ks2 = 1;
+  mlp_geometry(1, d, F, ks2);
+  return (size_t)MLP_HDR * sizeof(int) + mlp_hx_bytes(F) + (size_t)MLP_CNT * sizeof(int) +
+         (size_t)((d + 15) / 16) * ks2 * 512 * sizeof(float);
 }
 
 extern "C" size_t kw_dec_mlp_status_offset(int64_t M, int64_t d, int64_t F) {
@@ -1416,8 +1325,8 @@ extern "C" size_t kw_dec_mlp_status_offset(int64_t M, int64_t d, int64_t F) {
 extern "C" int kw_dec_mlp(const kw_dec_mlp_args* a, kw_stream_t stream) {
   if (!a || !a->x || !a->fc1_w || !a->fc1_colsum || !a->fc2_w || !a->h || !a->hb || !a->workspace)
     return kw_set_error_msg(KW_EINVAL, "kw_dec_mlp: null pointer");
-  Geo g1, g2;
-  if (!mlp_geometry(a->M, a->d, a->F, g1, g2))
+  int ks2;
+  if (!mlp_geometry(a->M, a->d, a->F, ks2))
     return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_mlp: shape not covered (kw_dec_mlp_supported)");
   if (a->ldx < a->d || a->ldx % 8 != 0 || (uintptr_t)a->x % 16 != 0 || a->ldh < a->d)
     return kw_set_error_msg(KW_EINVAL, "kw_dec_mlp: ldx >= d (multiple of 8, x 16-B aligned), ldh >= d");
@@ -1438,7 +1347,9 @@ extern "C" int kw_dec_mlp(const kw_dec_mlp_args* a, kw_stream_t stream) {
   p1.M = (int)a->M;
   p1.N = (int)a->F;
   p1.K = (int)a->d;
-  p1.xlds = use_xlds(a->F, g1) ? 1 : 0;
+  p1.xlds = 0;
+  p1.zrows = 32;
+  char* ws = reinterpret_cast<char*>(a->workspace);
   DecP& p2 = m.f2;
   p2.W = reinterpret_cast<const bf16x8*>(a->fc2_w);
   p2.bias = a->fc2_bias;
@@ -1448,20 +1359,17 @@ extern "C" int kw_dec_mlp(const kw_dec_mlp_args* a, kw_stream_t stream) {
   p2.M = (int)a->M;
   p2.N = (int)a->d;
   p2.K = (int)a->F;
-  m.ws = reinterpret_cast<int*>(a->workspace);
-  m.hx = reinterpret_cast<char*>(a->workspace) + MLP_HDR * sizeof(int);
-  m.n1 = (int)(a->F / 32);
-  m.ks2 = g2.ks;
-  m.nw2 = g2.nw;
-  const size_t shm = std::max(x_lds_bytes_for((int)(a->d / 32), 1, p1.xlds != 0), (size_t)g2.ks * g2.nw * 2048);
-  static size_t attr = 0;
-  if (shm > attr) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dec_mlp_kernel),
-                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm);
-    if (e != hipSuccess) return kw_set_error(e);
-    attr = shm;
-  }
-  const unsigned grid = (unsigned)(m.n1 + (a->d + 15) / 16);
+  p2.xlds = 0;
+  p2.zrows = 32;
+  p2.cnt = reinterpret_cast<int*>(ws + MLP_HDR * sizeof(int) + mlp_hx_bytes(a->F));
+  p2.slab = reinterpret_cast<float*>(reinterpret_cast<char*>(p2.cnt) + MLP_CNT * sizeof(int));
+  int* hdr = reinterpret_cast<int*>(ws);
+  m.n1 = (int)(a->F / 16);
+  m.ncb2 = (int)((a->d + 15) / 16);
+  m.ks2 = ks2;
+  m.pub = MlpPub{ws + MLP_HDR * sizeof(int), hdr, hdr + MLP_FAULT, hdr + MLP_STATUS, hdr + MLP_DONE, m.ncb2 * ks2, m.n1};
+  const size_t shm = 32 * 24 * sizeof(bf16_t);  // the producer's 32 x 16 tile (row stride 24)
+  const unsigned grid = (unsigned)(m.n1 + m.ncb2 * ks2);
   hipLaunchKernelGGL(dec_mlp_kernel, dim3(grid), dim3(512), shm, (hipStream_t)stream, m);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KW_OK : kw_set_error(e);

@@ -497,8 +497,8 @@ def test_handoff_timeout_raises(gold, tiny16, block):
 
 
 def test_fused_mlp_generate_identical():
-    """The opt-in fused feed-forward block (WhisperEngine(fuse_mlp=True): kw_dec_mlp, h / hb bitwise the two
-    launches) gives exactly the greedy tokens of the default two-launch plan at the kotoba-whisper shape (d 1280,
+    """The fused feed-forward block (WhisperEngine(fuse_mlp=True): kw_dec_mlp, h within f32 summation order of the
+    two launches) gives exactly the greedy tokens of the two-launch plan at the kotoba-whisper shape (d 1280,
     F 5120; two decoder layers), with and without timestamps, and its launches really replace fc1 / fc2."""
     from kwhisper.engine import WhisperEngine
     from kwhisper.generation import KWhisperForConditionalGeneration

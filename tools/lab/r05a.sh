@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 crash() { [ "$1" -ge 124 ]; }
 timeout -k 10 240 python -u tools/dump_hipmel.py --out gpurun_out/c4_hipmel_features.npz > gpurun_out/r05a_dump.log 2>&1 || exit 1
 echo DUMP_OK
-timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread -k "dec_linear" > gpurun_out/r05a_kern.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q --timeout 120 --timeout-method thread -k "dec_linear or mlp" > gpurun_out/r05a_kern.log 2>&1
 rc=$?; echo "KERN rc=$rc"; crash $rc && exit 1
 timeout -k 10 700 python -u -m pytest -m gpu -x -v -s --timeout 300 --timeout-method thread \
   "tests/test_gpu_workloads.py::test_config3_fp32_generate_b32_bitexact" \
@@ -21,6 +21,12 @@ for r in 1 2; do
   for v in base lab lab2; do
     case $v in base) unset KWHISPER_LIB KWHISPER_TORCH_LIB ;; *) export KWHISPER_LIB=$PWD/build_$v/libkwhisper.so KWHISPER_TORCH_LIB=$PWD/build_$v/libkwhisper_torch.so ;; esac
     echo "$v $(timeout -k 10 120 python tools/kbench.py --reps 40 --only lm_head 2>/dev/null)" >> gpurun_out/r05a_lmh_ab.txt || exit 1
+  done
+done
+for r in 1 2; do
+  for v in base lab2; do
+    case $v in base) unset KWHISPER_LIB KWHISPER_TORCH_LIB ;; *) export KWHISPER_LIB=$PWD/build_$v/libkwhisper.so KWHISPER_TORCH_LIB=$PWD/build_$v/libkwhisper_torch.so ;; esac
+    echo "$v $(timeout -k 10 120 python tools/kbench.py --reps 40 --only mlp,fc1_ln_gelu,fc2_resid 2>/dev/null)" >> gpurun_out/r05a_lmh_ab.txt || exit 1
   done
 done
 for r in 1 2; do
