@@ -114,12 +114,17 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
   //    (the MFMA fragment pattern -- 16 rows x 64 B per load, every workgroup reading the same rows --
   //    is 2-3x slower to land from L2 than contiguous pieces).  LDS image: 32 rows of cpr 16-B chunks
   //    plus one pad chunk per row (odd row stride: the fragment reads are bank-conflict free).
+  // (a row-split chunk, H2 = false: the other 16-row chunk's workgroup -- blockIdx 80 apart, the same XCD -- reads the
+  // same weight slice, so it is loaded with the default policy and the second read can hit that XCD's L2; r04's nt
+  // loads fetched 1.23x the o / xo weights from memory, profiles/r04p_pmc_fetch.csv)
   bf16x8 w[NCB][KTM], a0[KTM], a1[KTM];
 #pragma unroll
   for (int c = 0; c < NCB; ++c)
 #pragma unroll
-    for (int u = 0; u < KTM; ++u)
-      w[c][u] = __builtin_nontemporal_load(p.W + ((int64_t)(cg * NCB + c) * nkt + min(kt0 + u, ktl)) * 64 + lane);
+    for (int u = 0; u < KTM; ++u) {
+      const bf16x8* src = p.W + ((int64_t)(cg * NCB + c) * nkt + min(kt0 + u, ktl)) * 64 + lane;
+      w[c][u] = H2 ? __builtin_nontemporal_load(src) : *src;
+    }
   const int wkt0 = (nkt * ks) / ksn, wkt1 = (nkt * (ks + 1)) / ksn;  // this workgroup's k-tiles
   const int cpr = (wkt1 - wkt0) * 4, cprp = cpr + 1;
   const bool xlds = !CONS && p.xlds;
