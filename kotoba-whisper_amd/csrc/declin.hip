@@ -175,7 +175,11 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     // the producers' fragments of this wave's k-tiles: one poll over their flags (lane l: flag 2 kt0 + l), then sc1
     // loads (written in this launch by other CUs); a poll that timed out turns the operands into NaN
     const int fidx = lane < 2 * (kt1 - kt0) ? 2 * kt0 + lane : -1;
+#if defined(KW_MLP_LAB) && (KW_MLP_LAB == 1 || KW_MLP_LAB == 3)
+    const bool ok = fidx >= -1;  // lab decomposition: no wait (results wrong, timing real)
+#else
     const bool ok = mlp_wait(pub.flags, fidx, lane, pub.status);
+#endif
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx, (short)0, nkt * 2048, 0x00020000);
 #pragma unroll
@@ -482,6 +486,11 @@ __device__ __forceinline__ bool mlp_wait(const int* flags, int fidx, int lane, i
 }
 
 __global__ __launch_bounds__(512) void dec_mlp_kernel(MlpArgs a) {
+#if defined(KW_MLP_LAB) && KW_MLP_LAB == 2
+  if ((int)blockIdx.x >= a.n1) return;  // lab decomposition: the fc1 role alone
+#elif defined(KW_MLP_LAB) && KW_MLP_LAB == 3
+  if ((int)blockIdx.x < a.n1) return;  // lab decomposition: the fc2 role alone (no waits)
+#endif
   if ((int)blockIdx.x < a.n1) {
     dec_linear_body<5, 1, true, KW_EPI_STORE, bf16_t, true>(a.f1, 1, blockIdx.x, 0, 8, a.pub);
   } else {
@@ -958,9 +967,10 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       red[slot][wave][c][1][lane] = c1[c];
     }
     lmh_barrier();  // (three red slots: a slot is rewritten two barriers after its readers passed)
-    // waves 0..2*NCB-1 each finish one 16 x 16 tile: wave-ordered sum, LayerNorm, bias, store
-    if (wave < 2 * LMH_NCB) {
-      const int c = wave >> 1, hh = wave & 1;
+    // the 2 x NCB 16 x 16 tiles of the group, one per wave (a launch of fewer waves -- K < 640 -- takes several per
+    // wave): wave-ordered sum, LayerNorm, bias, store
+    for (int t = wave; t < 2 * LMH_NCB; t += nw) {
+      const int c = t >> 1, hh = t & 1;
       f32x4 acc = red[slot][0][c][hh][lane];
       for (int w2 = 1; w2 < nw; ++w2) acc += red[slot][w2][c][hh][lane];
       const int n = (g * LMH_NCB + c) * 16 + (lane & 15);
