@@ -16,6 +16,6 @@ int kw_set_error_msg(int code, const char* msg) {
   return code;
 }
 
-extern "C" int kw_version(void) { return 109; }
+extern "C" int kw_version(void) { return 110; }
 
 extern "C" const char* kw_last_error(void) { return g_err; }

@@ -446,7 +446,11 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
   dec_linear_body<KTM, NCB, LNA, EPI, TC, false, H2>(p, ksn, blockIdx.x, blockIdx.y, blockDim.x >> 6, MlpPub{});
 }
 
+#ifdef KW_LAB_MLP
 // ---- fused decode MLP: fc1 (LayerNorm-fused, GELU) -> fc2 (+ residual) in ONE launch (kw_dec_mlp) ----
+// LAB ONLY (make EXTRA=-DKW_LAB_MLP; tools/lab/mlp_coresident.py): it lost to the two kw_dec_linear launches (r04's
+// fc2-concentrated design 19.8 vs 18.6 us; this co-resident one 22.4-23.3, profiles/r05b_mlp_decomposition.txt), so
+// libkwhisper.so does not carry it.
 // r05, co-resident roles: workgroups [0, n1) are fc1, one per 16 columns (dec_linear_body<5, 1,
 // LN, STORE, GELU>: 8 waves x 5 k-tiles, each activation fragment loaded straight from hb -- no LDS image, so the
 // launch needs no more LDS than its reduction buffers), each publishing its tile -- half of one of fc2's k-tiles --
@@ -498,6 +502,7 @@ __global__ __launch_bounds__(512) void dec_mlp_kernel(MlpArgs a) {
     dec_linear_body<5, 1, false, KW_EPI_RESID, float, false, true, true>(a.f2, a.ks2, j % a.ncb2, j / a.ncb2, 8, a.pub);
   }
 }
+#endif  // KW_LAB_MLP
 
 // More than 32 rows without a K split (prefill positions, beam rows): each workgroup keeps its
 // columns' weight fragments in registers and walks ``zper`` 32-row chunks.  (One z-slice per chunk
@@ -1300,6 +1305,9 @@ extern "C" int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed,
   return KW_OK;
 }
 
+#ifdef KW_LAB_MLP
+#include "../../tools/lab/kw_mlp_lab.h"
+
 // ---- kw_dec_mlp (dec_mlp_kernel): fc1 -> fc2 of a greedy decode step in one launch ----
 namespace {
 
@@ -1389,3 +1397,4 @@ extern "C" int kw_dec_mlp(const kw_dec_mlp_args* a, kw_stream_t stream) {
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? KW_OK : kw_set_error(e);
 }
+#endif  // KW_LAB_MLP

@@ -279,35 +279,6 @@ void dec_qkv_self(const Tensor& x, const Tensor& W, const optional<Tensor>& bias
   check(kw_dec_qkv_self(&a, stream_of(x)), w);
 }
 
-// ---- fused decode feed-forward block (LayerNorm-fused fc1 + GELU -> fc2 + residual) ----------------------
-// dims = [ldx, M, d, F, ldh]; hb is fc1's input AND the residual mirror fc2 updates (x == hb in the decode step)
-void dec_mlp(const Tensor& W1, const optional<Tensor>& b1, const Tensor& cs1, const Tensor& W2, const optional<Tensor>& b2,
-             Tensor& h, Tensor& hb, Tensor& workspace, std::vector<int64_t> dims, double ln_eps) {
-  const char* w = "kw_dec_mlp";
-  dev(W1, w), dev(b1, w), dev(cs1, w), dev(W2, w), dev(b2, w), dev(h, w), dev(hb, w), dev(workspace, w);
-  TORCH_CHECK_VALUE(dims.size() == 5, "kw_dec_mlp: dims must hold 5 integers");
-  TORCH_CHECK_VALUE(hb.scalar_type() == at::kBFloat16 && W1.scalar_type() == at::kBFloat16 &&
-                        W2.scalar_type() == at::kBFloat16 && h.scalar_type() == at::kFloat,
-                    "kw_dec_mlp takes a bf16 residual mirror, packed bf16 weights and an f32 residual");
-  kw_dec_mlp_args a{};
-  a.x = ptr(hb);
-  a.ldx = dims[0];
-  a.ln_eps = (float)ln_eps;
-  a.fc1_colsum = ptr<const float>(cs1);
-  a.fc1_w = ptr(W1);
-  a.fc1_bias = optr<const float>(b1);
-  a.fc2_w = ptr(W2);
-  a.fc2_bias = optr<const float>(b2);
-  a.h = ptr<float>(h);
-  a.hb = ptr(hb);
-  a.M = dims[1], a.d = dims[2], a.F = dims[3];
-  a.ldh = dims[4];
-  a.workspace = ptr(workspace);
-  a.ws_bytes = (size_t)workspace.numel() * workspace.element_size();
-  c10::DeviceGuard g(hb.device());
-  check(kw_dec_mlp(&a, stream_of(hb)), w);
-}
-
 void cross_attn_step(const Tensor& q, int64_t B, int64_t q_len, int64_t H, int64_t hd, const Tensor& k, const Tensor& v,
                      int64_t S, Tensor& out, Tensor& workspace) {
   const char* w = "kw_cross_attn_step";
@@ -431,11 +402,9 @@ int64_t workspace_bytes(std::string kind, std::vector<int64_t> d) {
   if (kind == "qkv_self") return (int64_t)kw_dec_qkv_self_workspace(n(0), n(1));
   if (kind == "xq_cross") return (int64_t)kw_dec_xq_cross_workspace(n(0), n(1), n(2), n(3));
   if (kind == "beam_logprobs") return (int64_t)kw_beam_logprobs_workspace(n(0));
-  if (kind == "mlp") return (int64_t)kw_dec_mlp_workspace(n(0), n(1), n(2));
   // byte offsets of the hand-off status words inside those workspaces (include/kwhisper.h)
   if (kind == "qkv_self_status") return (int64_t)kw_dec_qkv_self_status_offset(n(0), n(1));
   if (kind == "xq_cross_status") return (int64_t)kw_dec_xq_cross_status_offset(n(0), n(1), n(2), n(3));
-  if (kind == "mlp_status") return (int64_t)kw_dec_mlp_status_offset(n(0), n(1), n(2));
   if (kind == "cross_attn_status") return (int64_t)kw_cross_attn_status_offset(n(0), n(1), n(2), n(3), n(4));
   TORCH_CHECK_VALUE(false, "kw::workspace_bytes: unknown kind ", kind);
 }
@@ -463,8 +432,6 @@ TORCH_LIBRARY(kw, m) {
         "Tensor cur_len, Tensor(c!) out, Tensor(d!) workspace, int[] dims, float ln_eps, float scale) -> ()");
   m.def("dec_xq_cross(Tensor x, Tensor W, Tensor? bias, Tensor ln_colsum, Tensor k, Tensor v, Tensor(a!) out, "
         "Tensor(b!) workspace, int[] dims, float ln_eps, float scale) -> ()");
-  m.def("dec_mlp(Tensor W1, Tensor? b1, Tensor cs1, Tensor W2, Tensor? b2, Tensor(a!) h, Tensor(b!) hb, "
-        "Tensor(c!) workspace, int[] dims, float ln_eps) -> ()");
   m.def("cross_attn_step(Tensor q, int B, int q_len, int H, int hd, Tensor k, Tensor v, int S, Tensor(a!) out, "
         "Tensor(b!) workspace) -> ()");
   m.def("greedy_step(Tensor(a!) logits, Tensor suppress_mask, Tensor? begin_suppress, Tensor(b!) ids, "
@@ -491,7 +458,6 @@ TORCH_LIBRARY_IMPL(kw, CUDA, m) {
   m.impl("cross_attn_step", &cross_attn_step);
   m.impl("dec_qkv_self", &dec_qkv_self);
   m.impl("dec_xq_cross", &dec_xq_cross);
-  m.impl("dec_mlp", &dec_mlp);
   m.impl("greedy_step", &greedy_step);
   m.impl("beam_logprobs", &beam_logprobs);
   m.impl("beam_select", &beam_select);

@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("KWHISPER_LIB") or os.path.join(os.path.dirname(os.pat
 TORCH_LIB_PATH = os.environ.get("KWHISPER_TORCH_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                       "libkwhisper_torch.so")
 TORCH_OPS = ("log_mel", "mel_to_time_major", "gemm", "dec_linear", "pack_weight", "layernorm", "attention", "embed",
-             "self_attn_step", "dec_qkv_self", "dec_xq_cross", "dec_mlp", "cross_attn_step", "greedy_step", "beam_logprobs", "beam_select")
+             "self_attn_step", "dec_qkv_self", "dec_xq_cross", "cross_attn_step", "greedy_step", "beam_logprobs", "beam_select")
 
 KW_OK, KW_EINVAL, KW_EHIP, KW_EUNSUPPORTED = 0, 1, 2, 3
 KW_DT_F32, KW_DT_BF16 = 0, 1
@@ -68,14 +68,6 @@ class XqCrossArgs(ctypes.Structure):
         ("x", c_vp), ("ldx", c_i64), ("ln_eps", ctypes.c_float), ("ln_colsum", c_vp), ("W", c_vp), ("bias", c_vp),
         ("scale", ctypes.c_float), ("M", c_i64), ("d", c_i64), ("H", c_i64), ("k", c_vp), ("v", c_vp),
         ("S", c_i64), ("out", c_vp), ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
-    ]
-
-
-class MlpArgs(ctypes.Structure):
-    _fields_ = [
-        ("x", c_vp), ("ldx", c_i64), ("ln_eps", ctypes.c_float), ("fc1_colsum", c_vp), ("fc1_w", c_vp),
-        ("fc1_bias", c_vp), ("fc2_w", c_vp), ("fc2_bias", c_vp), ("h", c_vp), ("hb", c_vp), ("ldh", c_i64),
-        ("M", c_i64), ("d", c_i64), ("F", c_i64), ("workspace", c_vp), ("ws_bytes", ctypes.c_size_t),
     ]
 
 
@@ -142,10 +134,6 @@ EXPORTS = {
     "kw_dec_xq_cross": (ctypes.c_int, [ctypes.POINTER(XqCrossArgs), c_vp]),
     "kw_dec_xq_cross_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64]),
     "kw_dec_xq_cross_supported": (ctypes.c_int, [c_i64, c_i64, c_i64, c_i64]),
-    "kw_dec_mlp": (ctypes.c_int, [ctypes.POINTER(MlpArgs), c_vp]),
-    "kw_dec_mlp_workspace": (ctypes.c_size_t, [c_i64, c_i64, c_i64]),
-    "kw_dec_mlp_supported": (ctypes.c_int, [c_i64, c_i64, c_i64]),
-    "kw_dec_mlp_status_offset": (ctypes.c_size_t, [c_i64, c_i64, c_i64]),
     "kw_cross_attn_pair_kernel": (ctypes.c_int, [c_i64, c_i64, ctypes.c_int]),
     "kw_dec_qkv_self_status_offset": (ctypes.c_size_t, [c_i64, c_i64]),
     "kw_dec_xq_cross_status_offset": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64]),

@@ -88,12 +88,6 @@ class DecodeSession:
                       and ops.xq_cross_supported(R, d, H, self.T))
         self.xc_ws = torch.zeros(((ops.xq_cross_workspace_bytes(R, d, H, self.T) + 3) // 4,), device=dev,
                                  dtype=torch.float32) if self.xc_ok else None
-        # fused feed-forward block (kw_dec_mlp): greedy rows, the large-v3 / kotoba-whisper FFN shape; h and hb
-        # bitwise the two-launch plan's
-        self.mlp_ok = (eng.packed and beams == 1 and getattr(eng, "fuse_mlp", False) and R <= 32
-                       and ops.mlp_supported(R, d, s.decoder_ffn_dim))
-        self.mlp_ws = torch.zeros(((ops.mlp_workspace_bytes(R, d, s.decoder_ffn_dim) + 3) // 4,), device=dev,
-                                  dtype=torch.float32) if self.mlp_ok else None
         self._graph = None
         self._graph_key = None
         self._cross_key = None
@@ -127,8 +121,8 @@ class DecodeSession:
         v._bufs, v._plans = {}, {}
         v.lin_ws = torch.zeros_like(self.lin_ws) if self.lin_ws is not None else None
         v.self_ws = torch.zeros_like(self.self_ws)
-        v.qs_ok = v.xc_ok = v.mlp_ok = False
-        v.qs_ws = v.xc_ws = v.mlp_ws = None
+        v.qs_ok = v.xc_ok = False
+        v.qs_ws = v.xc_ws = None
         return v
 
     def _prefill_parts(self, parts: int):
@@ -229,15 +223,10 @@ class DecodeSession:
                     seq.append(("cross", q, b["qx"], li, b["attn"], b["ws"]))
                 seq.append(lin(b["attn"], lay["xo_w"], rows, d, d, bias=lay["xo_b"], resid=(h, hb, d, 0),
                                workspace=ws, tag="xo"))
-                if q == 1 and self.mlp_ok:
-                    seq.append(ops.MlpPlan(h, hb, lay["fc1_w"], lay["fc2_w"], rows, d, s.decoder_ffn_dim,
-                                           ln=(eps, lay["fc1_cs"]), bias1=lay["fc1_b"], bias2=lay["fc2_b"],
-                                           workspace=self.mlp_ws))
-                else:
-                    seq.append(lin(hb, lay["fc1_w"], rows, s.decoder_ffn_dim, d, ln=(eps, lay["fc1_cs"]),
-                                   bias=lay["fc1_b"], C=b["ffn"], gelu=True, workspace=ws, tag="fc1"))
-                    seq.append(lin(b["ffn"], lay["fc2_w"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
-                                   resid=(h, hb, d, 0), workspace=ws, tag="fc2"))
+                seq.append(lin(hb, lay["fc1_w"], rows, s.decoder_ffn_dim, d, ln=(eps, lay["fc1_cs"]),
+                               bias=lay["fc1_b"], C=b["ffn"], gelu=True, workspace=ws, tag="fc1"))
+                seq.append(lin(b["ffn"], lay["fc2_w"], rows, d, s.decoder_ffn_dim, bias=lay["fc2_b"],
+                               resid=(h, hb, d, 0), workspace=ws, tag="fc2"))
             # final LayerNorm (folded into the packed LM head) + proj_out on the last position of every row
             seq.append(lin(hb, eng.lm_w, B, s.vocab_size, d, ldx=q * d, x_offset=(q - 1) * d,
                            ln=(eps, eng.lm_cs), bias=eng.lm_b, C=self.logits, workspace=ws, tag="lm_head"))
@@ -297,8 +286,6 @@ class DecodeSession:
             out.append(("kw_dec_qkv_self", self.qs_ws, ops.status_offset("qkv_self", self.R, s.d_model)))
         if self.xc_ws is not None:
             out.append(("kw_dec_xq_cross", self.xc_ws, ops.status_offset("xq_cross", self.R, s.d_model, H, self.T)))
-        if self.mlp_ws is not None:
-            out.append(("kw_dec_mlp", self.mlp_ws, ops.status_offset("mlp", self.R, s.d_model, s.decoder_ffn_dim)))
         for q, b in self._bufs.items():
             out.append(("kw_cross_attn_step", b["ws"], ops.status_offset("cross_attn", self.B, q * self.nb, H, _HD,
                                                                          self.T)))

@@ -63,7 +63,7 @@ class WhisperEngine:
 
     def __init__(self, shape: WhisperShape, state_dict: dict, *, dtype=torch.bfloat16, device="cuda",
                  generation_config: GenerationConstants | None = None, fuse_qkv_self: bool = True,
-                 fuse_xq_cross: bool = True, fuse_mlp: bool = False, encoder_streams: int = 2, prefill_streams: int = 2,
+                 fuse_xq_cross: bool = True, encoder_streams: int = 2, prefill_streams: int = 2,
                  steps_per_replay: int = 2):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
@@ -77,11 +77,8 @@ class WhisperEngine:
         # ... and each layer's cross-attention query projection + cross-attention step as one kw_dec_xq_cross launch
         # (bitwise the two-launch plan; False keeps the two launches)
         self.fuse_xq_cross = bool(fuse_xq_cross)
-        # ... and each layer's fc1 -> fc2 as one kw_dec_mlp launch (h and hb bitwise the two-launch plan; the shapes
-        # kw_dec_mlp_supported covers).  Off by default: measured 19.8 vs 18.6 us for the two launches at large-v3
-        # B = 32 (profiles/r04j_mlp_kbench.json; each fc2 workgroup's 320 KB activation read through L2 costs more
-        # than the boundary and weight round trip the fusion removes)
-        self.fuse_mlp = bool(fuse_mlp)
+        # (fc1 -> fc2 stays two launches: both fused designs lost -- r04's 19.8 and r05's co-resident 22.4-23.3 vs
+        # 18.4-18.6 us; the lab keeps them, tools/lab/mlp_coresident.py, profiles/r05b_mlp_decomposition.txt)
         # the encoder's batch as this many parts, their kernels issued interleaved on as many side streams: each
         # GEMM's last round of 256-row tiles leaves CUs idle that the other part's kernels fill (rows are
         # independent, so the output is bitwise the one-pass encoder's; large-v3 B = 32: 70.5 -> 67.6 ms,

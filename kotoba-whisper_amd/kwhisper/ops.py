@@ -73,8 +73,7 @@ def _ws_bytes(kind: str, *dims) -> int:
           "self_attn": "kw_self_attn_workspace", "cross_attn": "kw_cross_attn_workspace",
           "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace",
           "qkv_self": "kw_dec_qkv_self_workspace", "xq_cross": "kw_dec_xq_cross_workspace",
-          "qkv_self_status": "kw_dec_qkv_self_status_offset", "mlp": "kw_dec_mlp_workspace",
-          "mlp_status": "kw_dec_mlp_status_offset", "xq_cross_status": "kw_dec_xq_cross_status_offset",
+          "qkv_self_status": "kw_dec_qkv_self_status_offset", "xq_cross_status": "kw_dec_xq_cross_status_offset",
           "cross_attn_status": "kw_cross_attn_status_offset"}[kind]
     return int(getattr(_lib(), fn)(*dims))
 
@@ -429,57 +428,13 @@ class XqCrossPlan:
             L.check(_lib().kw_dec_xq_cross(self._ref, _s()), "kw_dec_xq_cross")
 
 
-def mlp_workspace_bytes(M, d, F) -> int:
-    return _ws_bytes("mlp", M, d, F)
-
-
-def mlp_supported(M, d, F) -> bool:
-    """Whether kw_dec_mlp covers the shape (M <= 32 rows; the large-v3 / kotoba-whisper FFN, d 1280, F 5120)."""
-    return bool(_lib().kw_dec_mlp_supported(int(M), int(d), int(F)))
-
-
-class MlpPlan:
-    """A pre-built ``kw_dec_mlp`` call: the decode step's feed-forward block in one launch -- the LayerNorm-fused
-    fc1 + GELU and fc2 + residual, h and hb bitwise the two kw_dec_linear launches'.  ``hb`` [M][ldh] bf16 is fc1's
-    input and the residual mirror it updates with ``h`` [M][ldh] f32; ``W1`` / ``W2`` packed (fc1 gamma folded),
-    ``ln`` = (eps, colsum [F]); ``workspace`` zero-filled (mlp_workspace_bytes)."""
-
-    def __init__(self, h, hb, W1, W2, M, d, F, *, ln, bias1, bias2, workspace, ldh=None, tag="mlp"):
-        _cuda(h, hb, W1, W2, bias1, bias2, workspace)
-        eps, colsum = ln
-        _cuda(colsum)
-        if hb.dtype != torch.bfloat16 or W1.dtype != torch.bfloat16 or W2.dtype != torch.bfloat16 or h.dtype != torch.float32:
-            raise ValueError("kw_dec_mlp takes a bf16 residual mirror, packed bf16 weights and an f32 residual")
-        ldh = d if ldh is None else ldh
-        if workspace.numel() * workspace.element_size() < mlp_workspace_bytes(M, d, F):
-            raise ValueError("kw_dec_mlp workspace too small")
-        self.tag = tag
-        a = L.MlpArgs()
-        a.x, a.ldx, a.ln_eps, a.fc1_colsum = hb.data_ptr(), ldh, float(eps), colsum.data_ptr()
-        a.fc1_w, a.fc1_bias = W1.data_ptr(), bias1.data_ptr() if bias1 is not None else None
-        a.fc2_w, a.fc2_bias = W2.data_ptr(), bias2.data_ptr() if bias2 is not None else None
-        a.h, a.hb, a.ldh = h.data_ptr(), hb.data_ptr(), ldh
-        a.M, a.d, a.F = M, d, F
-        a.workspace, a.ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
-        self._a = a
-        self._ref = ctypes.byref(a)
-        self._keep = (h, hb, W1, W2, bias1, bias2, colsum, workspace)
-        self._targs = (W1, bias1, colsum, W2, bias2, h, hb, workspace, [ldh, M, d, F, ldh], float(eps))
-
-    def __call__(self):
-        if _BACKEND == "torch":
-            _kw().dec_mlp(*self._targs)
-        else:
-            L.check(_lib().kw_dec_mlp(self._ref, _s()), "kw_dec_mlp")
-
-
 def cross_attn_workspace_bytes(B, q_len, H, hd, S) -> int:
     return _ws_bytes("cross_attn", B, q_len, H, hd, S)
 
 
 def status_offset(kind: str, *dims) -> int:
     """Byte offset of the int32 hand-off status word inside the workspace of ``kind`` ("qkv_self",
-    "xq_cross", "mlp", "cross_attn"; the workspace's own dimensions).  The word after it (qkv_self, xq_cross, mlp) is the
+    "xq_cross", "cross_attn"; the workspace's own dimensions).  The word after it (qkv_self, xq_cross) is the
     fault-injection word (include/kwhisper.h)."""
     return _ws_bytes(f"{kind}_status", *dims)
 

@@ -44,7 +44,7 @@ def test_version(lib):
 
     with open(os.path.join(ROOT, "include", "kwhisper.h")) as f:
         want = int(re.search(r"int kw_version\(void\);\s*/\*\s*(\d+)\s*\*/", f.read()).group(1))
-    assert lib.kw_version() == want == 109
+    assert lib.kw_version() == want == 110
 
 
 def _c_layout(struct, fields):
@@ -63,7 +63,7 @@ def _c_layout(struct, fields):
 @pytest.mark.parametrize("cname,pyname", [("kw_gemm_args", "GemmArgs"), ("kw_sampler_args", "SamplerArgs"),
                                           ("kw_dec_linear_args", "DecLinearArgs"),
                                           ("kw_dec_qkv_self_args", "QkvSelfArgs"),
-                                          ("kw_dec_xq_cross_args", "XqCrossArgs"), ("kw_dec_mlp_args", "MlpArgs")])
+                                          ("kw_dec_xq_cross_args", "XqCrossArgs")])
 def test_struct_layout_matches_c(cname, pyname):
     from kwhisper import _lib
 

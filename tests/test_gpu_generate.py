@@ -494,28 +494,3 @@ def test_handoff_timeout_raises(gold, tiny16, block):
     assert int(ws.view(torch.int32)[off // 4 + 1]) == 0  # consumed by exactly one launch
     assert all(int(w.view(torch.int32)[o // 4]) == 0 for _, w, o in sess.status_words())  # re-armed
     np.testing.assert_array_equal(tiny16.generate(feats, **kw).cpu().numpy(), want)
-
-
-def test_fused_mlp_generate_identical():
-    """The fused feed-forward block (WhisperEngine(fuse_mlp=True): kw_dec_mlp, h within f32 summation order of the
-    two launches) gives exactly the greedy tokens of the two-launch plan at the kotoba-whisper shape (d 1280,
-    F 5120; two decoder layers), with and without timestamps, and its launches really replace fc1 / fc2."""
-    from kwhisper.engine import WhisperEngine
-    from kwhisper.generation import KWhisperForConditionalGeneration
-
-    sd = synthetic_state_dict(KOTOBA_V2, 0)
-    g = torch.Generator(device="cuda").manual_seed(3)
-    feats = torch.randn(5, KOTOBA_V2.num_mel_bins, KOTOBA_V2.n_frames, device="cuda", generator=g) * 0.5
-    eng = WhisperEngine(KOTOBA_V2, sd, dtype=torch.bfloat16, generation_config=generation_constants(KOTOBA_V2))
-    del sd
-    plain = KWhisperForConditionalGeneration(eng)
-    fused = KWhisperForConditionalGeneration(eng.lane())
-    fused.engine.fuse_mlp = True
-    for ts in (False, True):
-        kw = dict(language="ja", task="transcribe", max_length=48, return_timestamps=ts)
-        a = fused.generate(feats, **kw).cpu()
-        b = plain.generate(feats, **kw).cpu()
-        assert torch.equal(a, b), ts
-    tags = {getattr(p, "tag", None) for p in fused._sessions[(5, 1)]._step_plans(1, fused=True)}
-    assert "mlp" in tags and "fc1" not in tags, tags
-    assert "mlp" not in {getattr(p, "tag", None) for p in plain._sessions[(5, 1)]._step_plans(1, fused=True)}

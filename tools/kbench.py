@@ -105,18 +105,6 @@ def main():
             plans.append(ops.DecLinearPlan(hb, W, B, N, K, **kw))
         us = timeit(plans, a.reps)
         res[name] = {"us": round(us, 2), "GBps": round(N * K * 2 / us / 1e3, 1)}
-    if want("mlp"):  # the greedy step's feed-forward block: fc1 (LN, GELU) -> fc2 (+ residual) in one launch
-        n_bufs = 1 if a.warm else nl
-        W1 = [ops.pack_weight((torch.randn(F, d, device=dev) / d ** 0.5).bfloat16()) for _ in range(n_bufs)]
-        W2 = [ops.pack_weight((torch.randn(d, F, device=dev) / F ** 0.5).bfloat16()) for _ in range(n_bufs)]
-        cs1, b1, b2 = torch.zeros(F, device=dev), torch.zeros(F, device=dev), torch.zeros(d, device=dev)
-        hm, hbm = torch.zeros(B, d, device=dev), torch.zeros(B, d, device=dev, dtype=torch.bfloat16)
-        wsm = torch.zeros(ops.mlp_workspace_bytes(B, d, F) // 4, device=dev)
-        plans = [ops.MlpPlan(hm, hbm, W1[i], W2[i], B, d, F, ln=(1e-5, cs1), bias1=b1, bias2=b2, workspace=wsm)
-                 for i in range(n_bufs)]
-        us = timeit(plans, a.reps)
-        res["mlp"] = {"us": round(us, 2), "GBps": round(2 * F * d * 2 / us / 1e3, 1)}
-        del W1, W2, plans
     # attention kernels (and the fused decode blocks: kw_dec_xq_cross, kw_dec_qkv_self)
     if not any(want(n) for n in ("cross_attn", "xq_cross", "self_attn", "qkv_self")):
         print(json.dumps(res))

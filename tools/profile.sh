@@ -12,7 +12,7 @@ mkdir -p gpurun_out
 RAW=/tmp/kw_prof_${TAG}
 rm -rf "$RAW"
 mkdir -p "$RAW"
-ONLY=cross_attn,xq_cross,self_attn,qkv_self,o_resid,fc1_ln_gelu,fc2_resid,mlp,qkv_ln,xq_ln,lm_head
+ONLY=cross_attn,xq_cross,self_attn,qkv_self,o_resid,fc1_ln_gelu,fc2_resid,qkv_ln,xq_ln,lm_head
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$RAW/bench_prof" -o run -- python3 bench.py --no-cpu-baseline --steps 2 --warmup 1 > gpurun_out/${TAG}_bench_prof.log 2>&1
 python3 tools/rocpd_summary.py --stats "$RAW/bench_prof/run_results.db" gpurun_out/${TAG}_bench_kernel_stats.csv
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$RAW/pmc_fetch" -o run -- python3 tools/kbench.py --eager --reps 2 --only $ONLY > gpurun_out/${TAG}_pmc_fetch.log 2>&1
