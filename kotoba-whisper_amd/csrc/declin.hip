@@ -834,6 +834,7 @@ __global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
 constexpr int LMH_KTM = 5;   // k-tiles per wave
 constexpr int LMH_NCB = 2;   // column blocks per group
 constexpr int LMH_MAXG = 16; // column groups per workgroup (epilogue constants staged in LDS; host-checked)
+constexpr int LMH_ECJ = 4;   // epilogue-constant columns staged per thread (host-checked: 64 * waves * 4 >= 32 * groups)
 #ifndef KW_LMH_BUFS
 #define KW_LMH_BUFS 3  // weight groups in registers: two in flight beside the one being multiplied (2: one)
 #endif
@@ -877,13 +878,14 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   };
   // issue order = wait order (vmcnt retires in order): the epilogue constants and the activation fragments first,
   // then the first two groups' weights, so the LayerNorm phase waits on the activations alone
-  const int ncon = (g1 - g0) * LMH_NCB * 16;  // this run's columns: thread t < ncon stages column t
-  float con_cs, con_bn;
-  {
-    const int t = min(tid, ncon - 1);
+  const int ncon = (g1 - g0) * LMH_NCB * 16;  // this run's columns: thread t stages columns t + j * blockDim
+  float con_cs[LMH_ECJ], con_bn[LMH_ECJ];
+#pragma unroll
+  for (int j = 0; j < LMH_ECJ; ++j) {  // (clamped, not skipped: no load under a branch, host-checked coverage)
+    const int t = min(tid + j * (int)blockDim.x, ncon - 1);
     const int n = min(g0 * LMH_NCB * 16 + t, p.N - 1);
-    con_cs = p.ln_colsum[n];
-    con_bn = p.bias ? p.bias[n] : 0.f;
+    con_cs[j] = p.ln_colsum[n];
+    con_bn[j] = p.bias ? p.bias[n] : 0.f;
   }
   // activation fragments of this wave's k-range, once (rows lane&15 and 16 + lane&15)
   bf16x8 a0[LMH_KTM], a1[LMH_KTM];
@@ -902,10 +904,14 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
 #endif
   wload(g0, wa);
   wload(g0 + 1, wb);
-  if (tid < ncon) {
-    const int gi = tid / (LMH_NCB * 16), c = (tid / 16) % LMH_NCB, col = tid % 16;
-    econ[gi][c][0][col] = con_cs;
-    econ[gi][c][1][col] = con_bn;
+#pragma unroll
+  for (int j = 0; j < LMH_ECJ; ++j) {
+    const int t = tid + j * (int)blockDim.x;
+    if (t < ncon) {
+      const int gi = t / (LMH_NCB * 16), c = (t / 16) % LMH_NCB, col = t % 16;
+      econ[gi][c][0][col] = con_cs[j];
+      econ[gi][c][1][col] = con_bn[j];
+    }
   }
   // a wave with fewer than LMH_KTM k-tiles multiplies zero activations for the rest (exact: 0 x w adds +0), so the
   // loop's MFMAs carry no per-k-tile branch (whose joins made the compiler wait for every load in flight)
@@ -1251,7 +1257,8 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     return e == hipSuccess ? KW_OK : kw_set_error(e);
   }
   const bool lmh = lm_shape && (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && a->M <= KW_LMH_MAX_ROWS &&
-                   lmh_groups_per_wg(a->N) <= LMH_MAXG;
+                   lmh_groups_per_wg(a->N) <= LMH_MAXG &&
+                   64 * ((nkt + LMH_KTM - 1) / LMH_KTM) * LMH_ECJ >= lmh_groups_per_wg(a->N) * LMH_NCB * 16;
   // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each)
   const int64_t step = (g.ks == 1 || lmh) ? a->M : 32 * ZMAX;
   for (int64_t m0 = 0; m0 < a->M; m0 += step) {

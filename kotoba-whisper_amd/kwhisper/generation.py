@@ -79,6 +79,9 @@ class KWhisperForConditionalGeneration:
         self.generation_config = engine.generation_config
         self._sessions = {}
         self.stats = {}
+        # True: generate() also keeps every seek pass's decoded ids in stats["pass_ids"] (validation: a fixture of the
+        # engine's own multi-pass trajectory, tools/dump_hipmel.py)
+        self.record_pass_ids = False
         self._memo = None  # generate_multitask's per-batch encoder memo
         self._memo_count = 0
 
@@ -239,6 +242,7 @@ class KWhisperForConditionalGeneration:
         last_ids = None
         passes = 0
         row_passes = np.zeros(B, dtype=np.int64)
+        pass_log, pass_ids = [], []  # per pass: (rows, their seek, their frame count); the decoded ids
         while (seek < max_frames).any():
             batch_map = [p for p in batch_map if seek[p] < max_frames[p]]
             cur = len(batch_map)
@@ -286,6 +290,10 @@ class KWhisperForConditionalGeneration:
                                     return_timestamps=return_timestamps)
             passes += 1
             last_ids = ids
+            pass_log.append(([int(p) for p in batch_map], [int(seek[p]) for p in batch_map],
+                             [int(seek_num[p]) for p in batch_map]))
+            if self.record_pass_ids:
+                pass_ids.append(np.asarray(ids).copy())
             pad, eos = gen.pad_token_id, gen.eos_token_id
             for i, p in enumerate(batch_map):
                 seq = ids[i, P:]
@@ -300,7 +308,9 @@ class KWhisperForConditionalGeneration:
                 segs, off = _retrieve_segment(seq, ts_begin, int(seek_num[p]), float(time_offset[p]))
                 seek[p] += off
                 segments[p] += segs
-        self.stats = {"passes": passes, "row_passes": row_passes}
+        self.stats = {"passes": passes, "row_passes": row_passes, "pass_log": pass_log}
+        if self.record_pass_ids:
+            self.stats["pass_ids"] = pass_ids
         if return_dict_in_generate and not return_timestamps:
             return {"sequences": torch.from_numpy(last_ids).to(eng.device)}
         seqs = [np.concatenate([x["tokens"] for x in segs]) if segs else np.zeros(0, np.int64) for segs in segments]

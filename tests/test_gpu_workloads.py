@@ -683,6 +683,57 @@ def test_config4_hipmel_multipass(gold):
     _free()
 
 
+@pytest.mark.parametrize("tag,floor", [("bf16", MARGIN_FLOOR), ("fp32", 1e-3)])
+def test_config4_hipmel_engine_trajectory(gold, tag, floor):
+    """Config 4's multi-pass case on the product's own inputs, along the ENGINE's trajectory.
+    transformers decodes the HIP log-mel fixture in one seek pass per row; the bf16 engine follows fp32's choices
+    only where fp32's margin exceeds the bf16 noise and so takes its own passes (up to three: a re-encode of the mel
+    shifted to its last timestamp, generation_whisper.py:785-903, the cumulative max_length :1935-1940).
+    tests/golden/large_v3_c4_hipmel_traj.npz holds the engine's passes recorded on the GPU box
+    (tools/dump_trajectory.py) and transformers' fp32 choice and margin at every step of them, teacher-forced
+    (tools/make_fixtures.py --only c4_traj).  The engine must reproduce its recorded passes exactly (rows, seek,
+    frames, ids: deterministic), and at every step where fp32 decides by at least ``floor`` its token must be fp32's
+    choice -- in every pass, the re-encoded later ones included."""
+    g, t = gold("large_v3_c4_hipmel"), gold("large_v3_c4_hipmel_traj")
+    if f"{tag}_pass_seq" not in t:
+        pytest.skip(f"no {tag} trajectory in the fixture")
+    feats = torch.from_numpy(g["features"]).cuda()
+    m = _model(LARGE_V3, torch.bfloat16 if tag == "bf16" else torch.float32)
+    m.record_pass_ids = True
+    toks = m.generate(feats, **C4_KW).cpu().numpy()
+    st = m.stats
+    np.testing.assert_array_equal(st["row_passes"], t[f"{tag}_passes"])
+    np.testing.assert_array_equal(toks, t[f"{tag}_tokens"])
+    rows = [r for rr, _, _ in st["pass_log"] for r in rr]
+    seeks = [x for _, ss, _ in st["pass_log"] for x in ss]
+    nfr = [x for _, _, nn in st["pass_log"] for x in nn]
+    np.testing.assert_array_equal(rows, t[f"{tag}_pass_row"])
+    np.testing.assert_array_equal(seeks, t[f"{tag}_pass_seek"])
+    np.testing.assert_array_equal(nfr, t[f"{tag}_pass_nframes"])
+    seqs = [x for ids in st["pass_ids"] for x in ids]
+    P = 3
+    n_cmp = n_tot = n_cmp2 = n_tot2 = 0
+    bad = []
+    for k, x in enumerate(seqs):
+        want = t[f"{tag}_pass_seq"][k]
+        np.testing.assert_array_equal(x, want[: len(x)])
+        n = int(t[f"{tag}_pass_len"][k])
+        safe = t[f"{tag}_hf_margin"][k, :n] >= floor
+        diff = np.nonzero(safe & (x[P: P + n] != t[f"{tag}_hf_choice"][k, :n]))[0]
+        bad += [(k, int(d)) for d in diff]
+        n_cmp += int(safe.sum())
+        n_tot += n
+        if t[f"{tag}_pass_iter"][k] >= 1:
+            n_cmp2 += int(safe.sum())
+            n_tot2 += n
+    print(f"\nconfig4 HIP log-mel, {tag} engine trajectory: passes per row {st['row_passes'].tolist()}; {n_cmp} of "
+          f"{n_tot} steps with transformers-fp32 margin >= {floor} compared (passes >= 2: {n_cmp2} of {n_tot2}), "
+          f"{len(bad)} differ from fp32's choice")
+    assert not bad, f"(pass entry, step) pairs off transformers' fp32 choice: {bad[:8]}"
+    del m
+    _free()
+
+
 @pytest.mark.parametrize("fixture", ["large_v3_longform_fp32", "large_v3_longform8_fp32"])
 def test_large_v3_longform_multipass(gold, fixture):
     """The seek loop's second and later passes at large-v3.  No config-4 stand-in clip takes a

@@ -450,6 +450,66 @@ def large_config4_hipmel_fixtures(features_npz, bf16=True):
     print(f"large_v3_c4_hipmel fixtures done in {time.time() - t0:.1f}s {toks.shape}")
 
 
+def large_config4_traj_fixtures(traj_npz):
+    """tests/golden/large_v3_c4_hipmel_traj.npz: transformers' fp32 large-v3 scoring the ENGINE's own seek passes on
+    the config-4 HIP log-mel fixture.  transformers decodes those features in one pass per row, the
+    bf16 engine in up to three (its greedy choice follows fp32's only where fp32's margin exceeds the bf16 noise).
+    ``traj_npz`` (tools/dump_trajectory.py, GPU box) holds every engine pass: rows, seek, frame count, ids.  For each
+    pass the segment input is rebuilt from the fixture's features exactly as generation_whisper.py:1831-1850 cuts it,
+    encoded by transformers, and the pass's ids fed through its decoder (teacher forcing); the logits are processed
+    as the reference's greedy step processes them (oracle.generate.process_logits: Suppress -> SuppressAtBegin ->
+    WhisperTimeStamp, pinned to transformers by tests/test_oracle_golden.py) and reduced to fp32's choice and its
+    top-1 / top-2 margin at every step of the engine's trajectory."""
+    sys.path.insert(0, ROOT)
+    from oracle.generate import process_logits
+
+    t0 = time.time()
+    g = np.load(os.path.join(GOLD, "large_v3_c4_hipmel.npz"))
+    tr = np.load(traj_npz)
+    feats = torch.from_numpy(g["features"].astype(np.float32))
+    m = hf_model(LARGE_V3)
+    gd = generation_constants(LARGE_V3).to_dict()
+    eos, P = gd["eos_token_id"], 3
+    out = {}
+    for tag in ("bf16", "fp32"):
+        if f"{tag}_pass_seq" not in tr.files:
+            continue
+        seq_all = tr[f"{tag}_pass_seq"]
+        n_ent, T = seq_all.shape
+        choice = np.full((n_ent, T - P), -1, np.int64)
+        margin = np.full((n_ent, T - P), np.inf, np.float32)
+        length = np.zeros(n_ent, np.int64)
+        for it in np.unique(tr[f"{tag}_pass_iter"]):
+            ks = np.nonzero(tr[f"{tag}_pass_iter"] == it)[0]
+            seg = torch.zeros((len(ks), feats.shape[1], 3000))
+            for i, k in enumerate(ks):
+                r, s0, nf = int(tr[f"{tag}_pass_row"][k]), int(tr[f"{tag}_pass_seek"][k]), int(tr[f"{tag}_pass_nframes"][k])
+                seg[i, :, :nf] = feats[r, :, s0: s0 + nf]
+            seq = seq_all[ks].copy()
+            for i, k in enumerate(ks):  # generated steps: up to and including the first EOS
+                body = seq[i, P:]
+                valid = body[body >= 0]
+                e = np.nonzero(valid == eos)[0]
+                length[k] = int(e[0]) + 1 if e.size else len(valid)
+            seq[seq < 0] = eos
+            L = int(P + length[ks].max())
+            with torch.no_grad():
+                enc = m.model.encoder(seg).last_hidden_state
+                lg = m(encoder_outputs=(enc,), decoder_input_ids=torch.from_numpy(seq[:, : L - 1])).logits.float().numpy()
+            for i, k in enumerate(ks):
+                for t in range(int(length[k])):
+                    sc = process_logits(seq[i: i + 1, : P + t], lg[i, P - 1 + t][None], gd, P, True)[0]
+                    top2 = np.partition(sc, -2)[-2:]
+                    choice[k, t] = int(sc.argmax())
+                    margin[k, t] = float(top2.max() - top2.min())
+            print(f"  c4_traj {tag}: pass {it} ({len(ks)} rows) scored ({time.time() - t0:.1f}s)", flush=True)
+        out.update({f"{tag}_{k}": tr[f"{tag}_{k}"] for k in ("tokens", "passes", "pass_iter", "pass_row", "pass_seek",
+                                                             "pass_nframes", "pass_seq")})
+        out.update({f"{tag}_pass_len": length, f"{tag}_hf_choice": choice, f"{tag}_hf_margin": margin})
+    np.savez_compressed(os.path.join(GOLD, "large_v3_c4_hipmel_traj.npz"), **out)
+    print(f"large_v3_c4_hipmel_traj fixtures done in {time.time() - t0:.1f}s")
+
+
 LARGE_LONG_CLIPS = [("tone", 0, 45.0), ("dummy", 3, 70.0)]
 # r04: eight more > 30 s clips (33-88 s) in one batch -- the multi-pass path on >= 8 rows (VERDICT r3 item 1)
 LARGE_LONG8_CLIPS = [("tone", 1, 38.0), ("dummy", 4, 52.0), ("tone", 2, 61.0), ("dummy", 5, 33.0),
@@ -621,6 +681,8 @@ def main():
     ap.add_argument("--hipmel", default="gpurun_out/c4_hipmel_features.npz",
                     help="--only c4_hipmel: tools/dump_hipmel.py output (the box's HIP log-mel of the chosen clips)")
     ap.add_argument("--no-bf16", action="store_true", help="--only c4_hipmel: skip the bf16 reference run")
+    ap.add_argument("--traj", default="gpurun_out/c4_traj.npz",
+                    help="--only c4_traj: tools/dump_trajectory.py output (the engine's seek passes on the fixture)")
     a = ap.parse_args()
     os.makedirs(GOLD, exist_ok=True)
     torch.manual_seed(0)
@@ -663,6 +725,8 @@ def main():
         large_longform_fixtures("large_v3_longform8_fp32", LARGE_LONG8_CLIPS)
     if not a.skip_large and a.only == "c4_hipmel":
         large_config4_hipmel_fixtures(a.hipmel, bf16=not a.no_bf16)
+    if not a.skip_large and a.only == "c4_traj":
+        large_config4_traj_fixtures(a.traj)
     if not a.skip_large and a.only in (None, "kotoba_beam"):
         kotoba_beam_fixtures()
     if a.only in (None, "pipeline"):
