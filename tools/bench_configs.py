@@ -52,10 +52,11 @@ def config4(a, world, rank, dev):
     from kwhisper.feature_extraction import WhisperFeatureExtractor
     from kwhisper.generation import KWhisperForConditionalGeneration
     from kwhisper.pseudo_label import pseudo_label, step_model
-    from kwhisper.synthetic import synthetic_state_dict_torch
+    from kwhisper.synthetic import synthetic_state_dict, synthetic_state_dict_torch
 
     shape = PRESETS["large-v3"]
-    sd = synthetic_state_dict_torch(shape, seed=0, device=dev)
+    # the weights decide the seek passes (timestamps): numpy = the model every transformers fixture pins
+    sd = synthetic_state_dict(shape, 0) if a.weights == "numpy" else synthetic_state_dict_torch(shape, seed=0, device=dev)
     model = KWhisperForConditionalGeneration.from_state_dict(shape, sd, dtype=torch.bfloat16, device=dev)
     del sd
     fe = WhisperFeatureExtractor(feature_size=shape.num_mel_bins, device=dev)
@@ -105,7 +106,7 @@ def config4(a, world, rank, dev):
             "dtype": "bf16", "data": "synthetic (ReazonSpeech-tiny duration statistics, noise audio, random weights)",
             "config": {"workload": "config 4: run_pseudo_labelling.py loop, whisper-large-v3, timestamps, greedy",
                        "per_gpu_batch": a.batch, "max_length": a.max_length, "parallelism": f"dp{world}",
-                       "gather": a.gather, "lanes": a.lanes, "schedule": a.schedule,
+                       "gather": a.gather, "lanes": a.lanes, "schedule": a.schedule, "weights": a.weights,
                        "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))},
             "batch_seconds": [round(float(x), 5) for x in batch_s], "batch_seek_passes": [passes[si] for si in sorted(passes)],
             "dp_projection": dp_projection(batch_s) if world == 1 and a.lanes == 1 else None}
@@ -192,6 +193,9 @@ def main():
     ap.add_argument("--max-length", type=int, default=128)
     ap.add_argument("--gather", choices=("round", "end"), default="end",
                     help="config 4: the reference's per-batch gather (round) or one exchange at the end")
+    ap.add_argument("--weights", choices=("numpy", "torch"), default="numpy",
+                    help="config 4: numpy = kwhisper.synthetic.synthetic_state_dict, the random model of the transformers "
+                    "fixtures (tests pin its seek passes); torch = the device generator's (another random model)")
     ap.add_argument("--schedule", choices=("static", "dynamic"), default="dynamic",
                     help="config 4 with --gather end: accelerate's batch-to-rank plan, or each batch to the first idle "
                     "rank (pseudo_label schedule='dynamic'; the same outputs)")

@@ -6,7 +6,8 @@ decodes in >= 2 passes of the timestamp seek loop (generation_whisper.py:785-903
 :1935-1940) are the ones transformers also re-encodes.  tools/make_fixtures.py --only large_c4 then builds the
 config-4 fixture over a 32-clip batch that contains such clips.
 
-    python tools/find_multipass.py --n-clips 640 --out gpurun_out/multipass.json
+    python tools/find_multipass.py --n-clips 1768 --weights numpy --out gpurun_out/multipass.json \
+        --features-out gpurun_out/multipass_features.npz
 """
 from __future__ import annotations
 
@@ -29,20 +30,27 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--out", default="gpurun_out/multipass.json")
+    ap.add_argument("--weights", choices=("numpy", "torch"), default="numpy",
+                    help="numpy: kwhisper.synthetic.synthetic_state_dict, the weights every transformers fixture uses; "
+                    "torch: synthetic_state_dict_torch (the device generator: a DIFFERENT random model, which "
+                    "transformers on the CPU cannot reproduce -- round 4's scan used it)")
+    ap.add_argument("--features-out", default="",
+                    help="npz of the HIP log-mel of every multi-pass clip (+ up to 8 one-pass clips) for "
+                    "tools/make_fixtures.py --only c4_hipmel")
     a = ap.parse_args()
     from kwhisper.config import LARGE_V3, generation_constants
     from kwhisper.feature_extraction import WhisperFeatureExtractor
     from kwhisper.generation import KWhisperForConditionalGeneration
-    from kwhisper.synthetic import reazon_audio, reazon_durations, synthetic_state_dict_torch
+    from kwhisper.synthetic import reazon_audio, reazon_durations, synthetic_state_dict, synthetic_state_dict_torch
 
     dev = torch.device("cuda", 0)
-    sd = synthetic_state_dict_torch(LARGE_V3, seed=0, device=dev)
+    sd = synthetic_state_dict(LARGE_V3, 0) if a.weights == "numpy" else synthetic_state_dict_torch(LARGE_V3, seed=0, device=dev)
     model = KWhisperForConditionalGeneration.from_state_dict(LARGE_V3, sd, dtype=getattr(torch, a.dtype), device=dev,
                                                              generation_config=generation_constants(LARGE_V3))
     del sd
     fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins, device=dev)
     durs = reazon_durations()[: a.n_clips]
-    passes, ntok = [], []
+    passes, ntok, keep = [], [], {}
     t0 = time.time()
     for b0 in range(0, len(durs), a.batch):
         idx = list(range(b0, min(b0 + a.batch, len(durs))))
@@ -53,18 +61,26 @@ def main():
         feats = fe.extract(torch.from_numpy(audio).to(dev))
         toks = model.generate(feats, language="ja", task="transcribe", return_timestamps=True, max_length=128)
         pad = model.generation_config.pad_token_id
-        passes += model.stats["row_passes"].tolist()
+        rp = model.stats["row_passes"].tolist()
+        for j, i in enumerate(idx):
+            if rp[j] >= 2 or (len(keep) < 8 and i < 8):
+                keep[i] = feats[j].cpu().numpy()
+        passes += rp
         ntok += (toks != pad).sum(1).cpu().tolist()
         print(f"batch {b0 // a.batch}: passes {model.stats['row_passes'].tolist()} ({time.time() - t0:.1f}s)",
               flush=True)
     passes = np.array(passes)
-    res = {"dtype": a.dtype, "n_clips": len(durs), "max_length": 128, "passes": passes.tolist(), "tokens": ntok,
+    if a.features_out and keep:
+        ids = sorted(keep)
+        np.savez_compressed(a.features_out, clip_ids=np.asarray(ids, np.int64), durations=durs[ids].astype(np.float64),
+                            features=np.stack([keep[i] for i in ids]).astype(np.float32))
+    res = {"dtype": a.dtype, "weights": a.weights, "n_clips": len(durs), "max_length": 128, "passes": passes.tolist(), "tokens": ntok,
            "multipass_clips": np.nonzero(passes >= 2)[0].tolist(),
            "histogram": {int(k): int((passes == k).sum()) for k in np.unique(passes)}}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(res, f)
-    print(json.dumps({k: res[k] for k in ("n_clips", "histogram")}), flush=True)
+    print(json.dumps({k: res[k] for k in ("dtype", "weights", "n_clips", "histogram", "multipass_clips")}), flush=True)
 
 
 if __name__ == "__main__":
