@@ -833,7 +833,7 @@ __global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
 #endif
 constexpr int LMH_KTM = 5;   // k-tiles per wave
 constexpr int LMH_NCB = 2;   // column blocks per group
-constexpr int LMH_MAXG = 16; // column groups per workgroup (epilogue constants staged in LDS; host-checked)
+constexpr int LMH_MAXG = 8;  // column groups per workgroup (epilogue constants and the logits staged in LDS; host-checked)
 constexpr int LMH_ECJ = 4;   // epilogue-constant columns staged per thread (host-checked: 64 * waves * 4 >= 32 * groups)
 #ifndef KW_LMH_BUFS
 #define KW_LMH_BUFS 3  // weight groups in registers: two in flight beside the one being multiplied (2: one)
@@ -852,6 +852,9 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   __shared__ float rpart[MAXW][32][2];
   __shared__ float rstat[32][2];
   __shared__ float econ[LMH_MAXG][LMH_NCB][2][16];  // [group][column block][colsum, bias][column]
+  // the run's logits, written back after the loop as whole row spans: a group's 16 x 16 tiles stored in place were
+  // 4 x 64-B pieces per wave instruction (rows 207 KB apart), 4 us of a 33 us launch (profiles/r05g_lmh_decomposition.txt)
+  __shared__ float obuf[32][LMH_MAXG * LMH_NCB * 16 + 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
   const int nkt = p.K >> 5;
   const int kt0 = (nkt * wave) / nw, kt1 = (nkt * (wave + 1)) / nw;  // <= LMH_KTM (host-checked)
@@ -963,6 +966,15 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
     __syncthreads();
   }
   // walk the run: groups g+1 and g+2 in flight while group g is multiplied, reduced and stored
+#if defined(KW_LMH_LAB) && KW_LMH_LAB == 2
+  uint32_t sink = 0;  // lab decomposition: the weight stream alone (no MFMA, barrier or epilogue)
+  auto body = [&](int g, int slot, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
+#pragma unroll
+    for (int c = 0; c < LMH_NCB; ++c)
+#pragma unroll
+      for (int u = 0; u < LMH_KTM; ++u) sink ^= __builtin_bit_cast(u32x4, w[c][u])[0];
+  };
+#else
   auto body = [&](int g, int slot, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
     f32x4 c0[LMH_NCB], c1[LMH_NCB];
 #pragma unroll
@@ -991,13 +1003,13 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
         for (int r = 0; r < 4; ++r) {
           const int m = 16 * hh + 4 * (lane >> 4) + r;
           if (m < M) {
-            const float v = rstat[m][1] * (acc[r] - rstat[m][0] * cs) + bn;
-            __builtin_nontemporal_store(v, reinterpret_cast<float*>(p.C) + (int64_t)m * p.ldc + n);
+            obuf[m][(g - g0) * LMH_NCB * 16 + c * 16 + (lane & 15)] = rstat[m][1] * (acc[r] - rstat[m][0] * cs) + bn;
           }
         }
       }
     }
   };
+#endif
 #if KW_LMH_BUFS == 3
   int g = g0;
   for (; g + 2 < g1; g += 3) {
@@ -1010,6 +1022,9 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   }
   if (g < g1) body(g, 0, wa);
   if (g + 1 < g1) body(g + 1, 1, wb);
+#if defined(KW_LMH_LAB) && KW_LMH_LAB == 2
+  if (sink == 0x12345678u) reinterpret_cast<float*>(p.C)[tid] = 0.f;
+#endif
 #else
   for (int g = g0 + 1; g < g1; g += 2) {  // (group g0 + 1 is already in flight)
     body(g - 1, 0, wa);
@@ -1018,6 +1033,20 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
     wload(g + 2, wb);
   }
   if ((g1 - g0) & 1) body(g1 - 1, 0, wa);
+#endif
+#if !defined(KW_LMH_LAB) || KW_LMH_LAB != 2
+  // the run's logits: row m's columns [32 g0, 32 g1) as one contiguous span (each wave instruction 64 consecutive
+  // floats = 256 B), non-temporal
+  lmh_barrier();
+  const int ncol = min(g1 * LMH_NCB * 16, p.N) - g0 * LMH_NCB * 16;
+  float* cbase = reinterpret_cast<float*>(p.C) + g0 * LMH_NCB * 16;
+  for (int i = tid; i < M * ncol; i += blockDim.x) {
+    const int m = i / ncol, col = i - m * ncol;
+#if defined(KW_LMH_LAB) && KW_LMH_LAB == 1
+    if (obuf[m][col] == 1234.5678f)  // lab decomposition: no logit stores (timing real, results wrong)
+#endif
+    __builtin_nontemporal_store(obuf[m][col], cbase + (int64_t)m * p.ldc + col);
+  }
 #endif
 }
 
