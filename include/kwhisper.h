@@ -29,8 +29,14 @@ enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
 enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 
 /* ABI version (major*100 + minor) and the last error message of this thread. */
-int kw_version(void);  /* 110 */
+int kw_version(void);  /* 111 */
 const char* kw_last_error(void);
+
+/* A new non-blocking stream of its own (hipStreamCreateWithFlags), for callers that must not share one: the streams a
+ * hipGraph capture forks into (PyTorch hands out streams from a fixed pool, so two host threads can be given the same
+ * one, and a thread's launches on a stream another thread's capture has forked into join that capture). */
+int kw_stream_create(kw_stream_t* out);
+int kw_stream_destroy(kw_stream_t stream);
 
 /* a1 -- log-mel spectrogram.
  * Replaces WhisperFeatureExtractor._torch_extract_fbank_features (TF/models/whisper/

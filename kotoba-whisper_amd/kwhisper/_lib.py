@@ -109,6 +109,8 @@ class BeamSelectArgs(ctypes.Structure):
 
 EXPORTS = {
     "kw_version": (ctypes.c_int, []),
+    "kw_stream_create": (ctypes.c_int, [ctypes.POINTER(c_vp)]),
+    "kw_stream_destroy": (ctypes.c_int, [c_vp]),
     "kw_last_error": (ctypes.c_char_p, []),
     "kw_log_mel": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp, c_vp, c_vp]),
     "kw_mel_to_time_major": (ctypes.c_int, [c_vp, c_i64, c_i64, c_i64, c_i64, c_vp, ctypes.c_int, c_vp]),
@@ -204,3 +206,22 @@ def check(rc: int, what: str) -> None:
         if rc == KW_EINVAL:
             raise ValueError(f"{what}: {msg}")
         raise KWError(f"{what} failed (code {rc}): {msg}")
+
+
+_OWN_STREAMS = []  # (raw handle, torch stream): kept for the process's lifetime
+
+
+def new_stream(device=None):
+    """A torch stream over a HIP stream of its own (``kw_stream_create``), not one of PyTorch's pooled streams: a pool
+    hands the same stream to two host threads once it wraps around, and a lane thread's launches on a stream that
+    another lane's hipGraph capture has forked into would join that capture ("capturing stream has unjoined work").
+    Every stream a capture uses or forks into comes from here."""
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    h = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        check(load().kw_stream_create(ctypes.byref(h)), "kw_stream_create")
+    s = torch.cuda.ExternalStream(h.value, device=dev)
+    _OWN_STREAMS.append((h, s))
+    return s

@@ -32,11 +32,18 @@ T_MAX = 448
 CAPTURE_LOCK = threading.RLock()
 
 
+_CAPTURE_STREAMS = {}  # device -> the stream every capture of the process runs on (captures are serialised)
+
+
 def capture_graph(fn, dev) -> torch.cuda.CUDAGraph:
-    """Capture ``fn``'s launches into a new graph on a side stream, under CAPTURE_LOCK."""
+    """Capture ``fn``'s launches into a new graph on a side stream of its own (L.new_stream: never a pooled stream
+    another thread may be launching on), under CAPTURE_LOCK."""
     with CAPTURE_LOCK:
         g = torch.cuda.CUDAGraph()
-        side = torch.cuda.Stream(device=dev)
+        key = torch.device(dev).index if torch.device(dev).index is not None else torch.cuda.current_device()
+        side = _CAPTURE_STREAMS.get(key)
+        if side is None:
+            side = _CAPTURE_STREAMS[key] = L.new_stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.graph(g, stream=side, capture_error_mode="thread_local"):
             fn()
@@ -135,7 +142,8 @@ class DecodeSession:
             for n in sizes:
                 views.append(self._row_view(r0, r0 + n))
                 r0 += n
-            self._plans[key] = (views, [torch.cuda.Stream(device=self.eng.device) for _ in range(parts)])
+            # (streams of their own: a captured prefill forks into them, L.new_stream)
+            self._plans[key] = (views, [L.new_stream(self.eng.device) for _ in range(parts)])
         return self._plans[key]
 
     def _run_prefill(self, P: int, parts: int) -> None:

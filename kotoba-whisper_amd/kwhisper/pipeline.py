@@ -27,6 +27,8 @@ from typing import Callable, Iterable, List, Optional, Sequence
 import numpy as np
 import torch
 
+from . import _lib
+
 from .config import LANGUAGES
 
 __all__ = ["chunk_iter", "find_longest_common_sequence", "decode_asr", "ASRPipeline"]
@@ -414,7 +416,7 @@ class ASRPipeline:
         import contextlib
         import threading
 
-        streams = [torch.cuda.Stream(device=torch.cuda.current_device()) for _ in range(n)] \
+        streams = [_lib.new_stream(torch.cuda.current_device()) for _ in range(n)] \
             if torch.cuda.is_available() else [None] * n
         errs = []
 

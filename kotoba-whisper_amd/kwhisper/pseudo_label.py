@@ -27,6 +27,8 @@ from typing import Callable, Iterable, List, Optional, Sequence
 import numpy as np
 import torch
 
+from . import _lib
+
 __all__ = ["shard_batches", "gather_remainder", "pad_across_processes", "gather_matrices", "pseudo_label",
            "pseudo_label_multitask", "last_schedule",
            "legacy_prompt", "write_transcription_csv", "transcription_table", "write_transcription_arrow"]
@@ -436,7 +438,7 @@ def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, com
     # each lane on its own stream of this rank's device (on one shared stream the lanes would serialise; a new
     # thread's current device is 0, the stream context sets it)
     n = len(decoders)
-    streams = [torch.cuda.Stream(device=torch.cuda.current_device()) for _ in range(n)] \
+    streams = [_lib.new_stream(torch.cuda.current_device()) for _ in range(n)] \
         if n > 1 and torch.cuda.is_available() else [None] * n
 
     def in_lane(i, work):
