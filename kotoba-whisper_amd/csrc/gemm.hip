@@ -301,6 +301,24 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b[j][ks], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
+  // group 0's read slot: its 8 A pieces for tile t+1 interleaved one per 3 fragment reads (r05: the pieces issued
+  // after all 24 reads left the slot longer; encoder 69.4-69.9 -> 68.8-69.0 ms, profiles/r05p_enc_ab.txt)
+  auto read_stage = [&](int buf, int tt, bool do_stage) {
+    const char* As = smem + buf * P_BUF + grp * 128 * 128;
+    const char* Bs = smem + buf * P_BUF + P_OP + wq * 64 * 128;
+    char* dst = smem + (buf ^ 1) * P_BUF + wq * 8 * 1024;
+    const char* src = sbase + (int64_t)tt * (PK * 2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (do_stage) glds16(src + soff[k], dst + k * 1024);
+#pragma unroll
+      for (int r = 3 * k; r < 3 * k + 3; ++r) {
+        if (r < 8) b[r >> 1][r & 1] = *reinterpret_cast<const bf16x8*>(Bs + (r >> 1) * 2048 + ((r & 1) ? rd1 : rd0));
+        else a[(r - 8) >> 1][(r - 8) & 1] = *reinterpret_cast<const bf16x8*>(As + ((r - 8) >> 1) * 2048 + (((r - 8) & 1) ? rd1 : rd0));
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
 
   // The residual epilogue reads C and row_add reads a table: those loads would queue behind the next
   // tile's prologue (vmcnt is in order), so such launches issue the prologue after the epilogue.
@@ -327,8 +345,7 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
     if (grp == 0) {
       for (int t = 0; t < nk; ++t) {
         const int buf = t & 1;
-        read_frags(buf);
-        if (t + 1 < nk) stage(t + 1, buf ^ 1);  // A of tile t+1 (its buffer's last reader finished in slot 2t-1)
+        read_stage(buf, t + 1, t + 1 < nk);  // + A of tile t+1 (its buffer's last reader finished in slot 2t-1)
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         pp_barrier();
         mma();
@@ -497,9 +514,14 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
             *c = o;
           } else {
             if (p.gelu) {
+#if defined(KW_GEMM_LAB) && KW_GEMM_LAB == 1
+#pragma unroll
+              for (int e = 0; e < VEC; ++e) v[e] = (v[e] + cadd[e]) * cmul[e];  // lab: the epilogue without GELU
+#else
 #pragma unroll
               for (int e = 0; e < VEC; ++e)
                 v[e] = (sizeof(TC) == 2 ? gelu_bf16out(v[e] + cadd[e]) : gelu_erf(v[e] + cadd[e])) * cmul[e];
+#endif
             } else {
 #pragma unroll
               for (int e = 0; e < VEC; ++e) v[e] = fmaf(v[e], cmul[e], cadd[e]);
@@ -526,6 +548,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
               // the out-proj / fc2 deltas stay cacheable for the HBM-bound LayerNorm that reads them next
               const bool nt = EPI == KW_EPI_HEADSPLIT || p.gelu;
               typedef __attribute__((ext_vector_type(4))) unsigned int nt_u4;
+#if defined(KW_GEMM_LAB) && KW_GEMM_LAB == 2
+              if (o.x == 0x12345678u)  // lab: the epilogue without its stores (timing real, results wrong)
+#endif
               if (nt)
                 __builtin_nontemporal_store(nt_u4{o.x, o.y, o.z, o.w}, reinterpret_cast<nt_u4*>(reinterpret_cast<bf16_t*>(p.C) + off));
               else

@@ -465,16 +465,20 @@ def test_lanes_checkpoint_resume(tmp_path):
 
 # ---- dynamic batch assignment (schedule="dynamic": list scheduling over a shared counter) -----
 class _SlowModel(_CountingModel):
-    """Batches holding an item of ``slow`` take ``delay`` seconds (a batch with extra seek passes)."""
+    """Batches holding an item of ``slow`` take ``delay`` seconds (a batch with extra seek passes); ``"first"`` in
+    ``slow`` makes the model's first batch slow, whichever batch its rank claimed first."""
 
     def __init__(self, slow=(), delay=0.0):
         super().__init__()
-        self.slow, self.delay = set(slow), delay
+        self.first = "first" in slow
+        self.slow, self.delay = {s for s in slow if s != "first"}, delay
+        self.calls = 0
 
     def generate(self, feats, **kw):
         import time
 
-        if self.slow & set(feats[:, 0].long().tolist()):
+        self.calls += 1
+        if (self.first and self.calls == 1) or self.slow & set(feats[:, 0].long().tolist()):
             time.sleep(self.delay)
         return super().generate(feats, **kw)
 
@@ -534,7 +538,8 @@ def test_dynamic_schedule_balances_a_slow_rank(tmp_path):
     import torch.multiprocessing as mp
 
     n, bs = 16, 2  # 8 batches
-    mp.spawn(_dynamic_worker, args=(2, _free_port(), n, bs, str(tmp_path), "", (0,), 1), nprocs=2, join=True)
+    # (rank 0's FIRST batch is the slow one: which batch a rank claims first is a race under dynamic claims)
+    mp.spawn(_dynamic_worker, args=(2, _free_port(), n, bs, str(tmp_path), "", ("first",), 1), nprocs=2, join=True)
     runs = [json.load(open(tmp_path / f"y{r}.json")) for r in range(2)]
     assert all(z["same"] for z in runs)
     assert len(runs[1]["decoded"]) >= 5, runs  # rank 0 spent 0.4 s on batch 0: rank 1 took (nearly) all the rest
