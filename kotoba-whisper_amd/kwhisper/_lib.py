@@ -9,6 +9,8 @@ process; both carry SONAME libamdhip64.so.7).
 from __future__ import annotations
 
 import ctypes
+import threading
+import weakref
 import os
 
 import torch  # noqa: F401  (must precede the library load: shared HIP runtime)
@@ -208,20 +210,39 @@ def check(rc: int, what: str) -> None:
         raise KWError(f"{what} failed (code {rc}): {msg}")
 
 
-_OWN_STREAMS = []  # (raw handle, torch stream): kept for the process's lifetime
+_OWN_STREAMS = []  # (raw handle, torch stream): every stream made here, kept for the process's lifetime
+_FREE_STREAMS = {}  # device index -> streams whose owner is gone, handed out again before a new one is made
+_STREAM_LOCK = threading.Lock()
 
 
-def new_stream(device=None):
+def new_stream(device=None, owner=None):
     """A torch stream over a HIP stream of its own (``kw_stream_create``), not one of PyTorch's pooled streams: a pool
     hands the same stream to two host threads once it wraps around, and a lane thread's launches on a stream that
     another lane's hipGraph capture has forked into would join that capture ("capturing stream has unjoined work").
-    Every stream a capture uses or forks into comes from here."""
+    Every stream a capture uses or forks into comes from here.  Streams are recycled, never destroyed: ``owner``
+    (an object) returns the stream when it is garbage collected, ``release_stream`` returns it explicitly; either
+    way it is handed out again only after that -- so repeated calls (sessions, lanes, pipeline calls) reuse streams
+    instead of making more."""
     import torch
 
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-    h = ctypes.c_void_p()
-    with torch.cuda.device(dev):
-        check(load().kw_stream_create(ctypes.byref(h)), "kw_stream_create")
-    s = torch.cuda.ExternalStream(h.value, device=dev)
-    _OWN_STREAMS.append((h, s))
+    with _STREAM_LOCK:
+        free = _FREE_STREAMS.setdefault(dev.index, [])
+        s = free.pop() if free else None
+    if s is None:
+        h = ctypes.c_void_p()
+        with torch.cuda.device(dev):
+            check(load().kw_stream_create(ctypes.byref(h)), "kw_stream_create")
+        s = torch.cuda.ExternalStream(h.value, device=dev)
+        with _STREAM_LOCK:
+            _OWN_STREAMS.append((h, s))
+    if owner is not None:
+        weakref.finalize(owner, release_stream, s)
     return s
+
+
+def release_stream(s) -> None:
+    """Hand a ``new_stream`` stream back (its owner is done with it; work already queued on it stays ordered ahead of
+    whatever its next user queues)."""
+    with _STREAM_LOCK:
+        _FREE_STREAMS.setdefault(s.device.index, []).append(s)

@@ -143,7 +143,7 @@ class DecodeSession:
                 views.append(self._row_view(r0, r0 + n))
                 r0 += n
             # (streams of their own: a captured prefill forks into them, L.new_stream)
-            self._plans[key] = (views, [L.new_stream(self.eng.device) for _ in range(parts)])
+            self._plans[key] = (views, [L.new_stream(self.eng.device, owner=self) for _ in range(parts)])
         return self._plans[key]
 
     def _run_prefill(self, P: int, parts: int) -> None:

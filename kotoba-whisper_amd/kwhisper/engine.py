@@ -301,7 +301,7 @@ class WhisperEngine:
             self._enc_split[key] = (out, bufs)
         out, bufs = self._enc_split[key]
         while len(self._enc_streams) < parts:
-            self._enc_streams.append(L.new_stream(self.device))
+            self._enc_streams.append(L.new_stream(self.device, owner=self))
         streams = self._enc_streams[:parts]
         cur = torch.cuda.current_stream(self.device)
         r0 = 0

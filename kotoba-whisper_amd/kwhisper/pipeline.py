@@ -433,6 +433,9 @@ class ASRPipeline:
             th.start()
         for th in threads:
             th.join()
+        for st in streams:  # (recycled by the next call's lanes: _lib.new_stream)
+            if st is not None:
+                _lib.release_stream(st)
         if errs:
             raise errs[0]
         return local

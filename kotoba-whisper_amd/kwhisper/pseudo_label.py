@@ -458,6 +458,9 @@ def _label_loop_deferred(model, features, n_items, batch_size, pad_token_id, com
             th.start()
         for th in threads:
             th.join()
+        for st in streams:  # (recycled by the next call's lanes: _lib.new_stream)
+            if st is not None:
+                _lib.release_stream(st)
         if errs:
             raise errs[0]
 

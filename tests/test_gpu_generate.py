@@ -494,3 +494,27 @@ def test_handoff_timeout_raises(gold, tiny16, block):
     assert int(ws.view(torch.int32)[off // 4 + 1]) == 0  # consumed by exactly one launch
     assert all(int(w.view(torch.int32)[o // 4]) == 0 for _, w, o in sess.status_words())  # re-armed
     np.testing.assert_array_equal(tiny16.generate(feats, **kw).cpu().numpy(), want)
+
+
+def test_own_streams_recycled():
+    """kwhisper._lib.new_stream (the HIP streams of their own that captures, prefill parts, encoder parts and lanes
+    use) hands a stream back out once its owner is garbage collected or it is released, instead of making more:
+    repeated sessions / lane calls do not grow the process's streams."""
+    import gc
+
+    from kwhisper import _lib as L
+
+    class Owner:
+        pass
+
+    n0 = len(L._OWN_STREAMS)
+    for _ in range(5):
+        o = Owner()
+        L.new_stream(owner=o)
+        del o
+        gc.collect()
+    assert len(L._OWN_STREAMS) <= n0 + 1
+    s1 = L.new_stream()
+    L.release_stream(s1)
+    assert L.new_stream() is s1
+    L.release_stream(s1)
