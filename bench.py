@@ -228,6 +228,7 @@ def main(argv=None):
     from kwhisper.feature_extraction import WhisperFeatureExtractor
     from kwhisper.generation import KWhisperForConditionalGeneration
     from kwhisper.synthetic import dummy_audio, synthetic_state_dict_torch
+    from kwhisper import _lib as L
     from kwhisper import ops
 
     shape = PRESETS[a.model]
@@ -291,7 +292,7 @@ def main(argv=None):
         import threading
 
         lanes = [KWhisperForConditionalGeneration(model.engine.lane()) for _ in range(n_lanes)]
-        streams = [torch.cuda.Stream(device=dev) for _ in lanes]
+        streams = [L.new_stream(dev) for _ in lanes]  # HIP streams of their own (kwhisper._lib.new_stream)
         ref = out_ids[-1].cpu()
         for m, st in zip(lanes, streams):
             with torch.cuda.stream(st):
