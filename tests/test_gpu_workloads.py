@@ -650,6 +650,23 @@ def _teacher_forced_per_pass(model, feats, g, floor=MARGIN_FLOOR):
     return n_cmp, n_tot, n_cmp2, n_tot2, bad
 
 
+def test_hipmel_fixture_features_reproduce(gold):
+    """The product's log-mel (kwhisper.WhisperFeatureExtractor on the GPU) of the fixture's stand-in clips, each
+    zero-padded to 30 s, is BITWISE the features tests/golden/large_v3_c4_hipmel.npz holds (dumped on the GPU box by
+    tools/dump_hipmel.py): the log-mel kernel's output is pinned, not only its tolerance to the oracle."""
+    from kwhisper.feature_extraction import WhisperFeatureExtractor
+    from kwhisper.synthetic import reazon_audio
+
+    g = gold("large_v3_c4_hipmel")
+    audio = np.zeros((len(g["clip_ids"]), 480000), np.float32)
+    for j, (i, d) in enumerate(zip(g["clip_ids"], g["durations"])):
+        c = reazon_audio(int(i), float(d))
+        audio[j, : len(c)] = c
+    fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins, device=torch.device("cuda", 0))
+    got = fe.extract(torch.from_numpy(audio).cuda()).cpu().numpy()
+    np.testing.assert_array_equal(got, g["features"])
+
+
 def test_config4_hipmel_multipass(gold):
     """Config 4 on the PRODUCT's own inputs: tests/golden/large_v3_c4_hipmel.npz holds the HIP
     log-mel that kwhisper.WhisperFeatureExtractor gave stand-in clips 1 and 522 (three seek passes in the round-4
