@@ -226,6 +226,8 @@ def new_stream(device=None, owner=None):
     import torch
 
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if dev.index is None:  # "cuda": the current device (free lists are keyed by index, as s.device.index)
+        dev = torch.device("cuda", torch.cuda.current_device())
     with _STREAM_LOCK:
         free = _FREE_STREAMS.setdefault(dev.index, [])
         s = free.pop() if free else None
