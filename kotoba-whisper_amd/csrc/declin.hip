@@ -549,8 +549,23 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
         a1[u] = *reinterpret_cast<const bf16x8*>(x + (int64_t)r1 * p.ldx + k);
       }
     }
+    // the residual values, loaded by the wave that writes them in the epilogue (NCB == 2: its job (c, hh))
     float hold[NCB][2][4];
-    if constexpr (EPI == KW_EPI_RESID) {
+    if constexpr (EPI == KW_EPI_RESID && NCB == 2) {
+#pragma unroll
+      for (int c = 0; c < NCB; ++c) {
+        const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh)
+          if ((2 * c + hh) % nw == wave) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int m = min(16 * hh + 4 * (lane >> 4) + r, M - 1);
+              hold[c][hh][r] = p.h[(int64_t)(m0 + m) * p.ldh + n];
+            }
+          }
+      }
+    } else if constexpr (EPI == KW_EPI_RESID) {
       if (wave == 0) {
 #pragma unroll
         for (int c = 0; c < NCB; ++c) {
@@ -607,7 +622,7 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
         rpart[wave][16 + (lane & 15)][1] = q1[di];
       }
     }
-    if (nw > 1) {
+    if (NCB == 2 || nw > 1) {
 #pragma unroll
       for (int c = 0; c < NCB; ++c) {
         red[wave][c][0][lane] = c0[c];
@@ -615,7 +630,58 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
       }
     }
     __syncthreads();
-    if (wave == 0) {
+    if constexpr (NCB == 2) {
+      // two column blocks: the epilogue's four jobs -- (column block c, row half hh) -- spread over the waves (job
+      // = wave + i nw), each summing its partial tiles over the waves in wave order as wave 0 alone does below and
+      // forming its row half's LayerNorm statistics itself (LDS is in order within a wave; two jobs of one half
+      // write the same values): bitwise the same results.  fc1 at 320 rows 41.4 -> 36.5 us; one column block keeps
+      // wave 0 alone, which measured faster there (profiles/r05al_rows_epilogue_ab.txt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int job = wave + i * nw;
+        if (job >= 4) break;
+        const int c = job >> 1, hh = job & 1;
+        if constexpr (LNA) {
+          if (lane < 16) {
+            const int m = 16 * hh + lane;
+            float sx = 0.f, sq = 0.f;
+            for (int w2 = 0; w2 < nw; ++w2) {
+              sx += rpart[w2][m][0];
+              sq += rpart[w2][m][1];
+            }
+            const float inv = 1.f / (float)p.K;
+            const float mean = sx * inv;
+            rstat[m][0] = mean;
+            rstat[m][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + p.ln_eps);
+          }
+        }
+        f32x4 acc = red[0][c][hh][lane];
+        for (int w2 = 1; w2 < nw; ++w2) acc += red[w2][c][hh][lane];
+        const int n = (cg * NCB + c) * 16 + (lane & 15);
+        const bool nvalid = n < p.N;
+        const float bn = ebias[c];
+        const float cs = ecsum[c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * hh + 4 * (lane >> 4) + r;
+          const bool valid = nvalid && m < M;
+          float v = acc[r];
+          if constexpr (LNA) v = rstat[m][1] * (v - rstat[m][0] * cs);
+          v += bn;
+          if constexpr (EPI == KW_EPI_RESID) {
+            v += hold[c][hh][r];
+            if (valid) {
+              p.h[(int64_t)(m0 + m) * p.ldh + n] = v;
+              p.hb[(int64_t)(m0 + m) * p.ldh + n] = f2bf(v);
+            }
+          } else {
+            if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
+            if (n < p.scale_cols) v *= p.scale;
+            if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)(m0 + m) * p.ldc + n, v);
+          }
+        }
+      }
+    } else if (wave == 0) {
       for (int w2 = 1; w2 < nw; ++w2)
 #pragma unroll
         for (int c = 0; c < NCB; ++c) {
