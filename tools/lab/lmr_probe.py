@@ -24,7 +24,8 @@ def main():
     W = ops.pack_weight((torch.randn(N, K, device=dev) / K ** 0.5).bfloat16())
     cs = torch.randn(N, device=dev)
     out = {}
-    for M in (32, 33, 64, 128, 192, 256, 320):
+    rows = [int(a) for a in sys.argv[1:]] or [32, 33, 64, 128, 192, 256, 320]  # (row counts on the command line)
+    for M in rows:
         x = (torch.randn(M, K, device=dev) * 0.5).bfloat16()
         C = torch.empty(M, N, device=dev)
         plan = ops.DecLinearPlan(x, W, M, N, K, ln=(1e-5, cs), C=C)
