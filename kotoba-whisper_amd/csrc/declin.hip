@@ -759,21 +759,26 @@ __device__ __forceinline__ void lmr_barrier() {  // raw s_barrier: no implicit v
   asm volatile("" ::: "memory");
 }
 
-template <int G>  // LDS-DMA pieces per wave per slice (= staged rows / 64)
-__global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
-  constexpr int NBUF = 3, PD = 8;  // activation slices in LDS (2 in flight), weight fragments in flight
-  __shared__ __attribute__((aligned(16))) char abuf[NBUF][LMR_MAXROWS * 64];  // 3 x 20 KB
+// NWV waves (16 columns each); G 16-B LDS-DMA pieces per lane per slice (a slice holds 16 NWV G rows); NZ 32-row
+// chunks computed.  NWV = 4: three slices (two staged ahead), two workgroups per CU; NWV = 8: five slices (four
+// staged ahead), one workgroup per CU -- the same eight waves per CU, each slice staged once per CU instead of twice.
+template <int NWV, int G, int NZ>
+__global__ __launch_bounds__(64 * NWV) void lm_head_rows_kernel(DecP p) {
+  constexpr int NBUF = NWV == 8 ? 5 : 3, LEAD = NBUF - 1, PD = 8;  // slices in LDS, weight fragments in flight
+  constexpr int SLICE = 1024 * NWV * G;                            // bytes per slice (64 B per row)
+  static_assert(NZ <= LMR_NZ && 32 * NZ <= 16 * NWV * G && PD > LEAD, "lm_head_rows_kernel geometry");
+  __shared__ __attribute__((aligned(16))) char abuf[NBUF][SLICE];
   __shared__ float rsum[LMR_MAXROWS], rsq[LMR_MAXROWS];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = p.M, nkt = p.K >> 5, nz = (M + 31) / 32;
   const int n_cb = (p.N + 15) / 16;
-  const int cb = min(blockIdx.x * 4 + wave, n_cb - 1);
+  const int cb = min(blockIdx.x * NWV + wave, n_cb - 1);
   // staging: piece j (16 B) = row j >> 2, LDS chunk j & 3, holding source chunk (j & 3) ^ ((row >> 2) & 3)
   auto stage = [&](int buf, int kt) {
     char* dst = abuf[buf];
 #pragma unroll
     for (int i = 0; i < G; ++i) {
-      const int j0 = wave * 64 + 256 * i;
+      const int j0 = wave * 64 + 64 * NWV * i;
       const int j = j0 + lane, row = j >> 2, ch = (j & 3) ^ ((row >> 2) & 3);
       glds16(p.x + (int64_t)min(row, M - 1) * p.ldx + kt * 32 + ch * 8, dst + j0 * 16);
     }
@@ -784,33 +789,36 @@ __global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
     acc0[z] = f32x4{0.f, 0.f, 0.f, 0.f};
     acc1[z] = acc0[z];
   }
-  // row statistics from the fragments: wave w sums chunks z = w, w + 4, w + 8 (slot z >> 2); lane
+  // row statistics from the fragments: wave w sums chunks z = w, w + NWV, ... (slot z / NWV); lane
   // (fr, fc) holds 8 values of rows 32z + fr and 32z + 16 + fr
-  constexpr int NSL = (LMR_NZ + 3) / 4;
+  constexpr int NSL = (LMR_NZ + NWV - 1) / NWV;
   float ss[NSL][2], sq[NSL][2];
 #pragma unroll
   for (int t = 0; t < NSL; ++t) ss[t][0] = ss[t][1] = sq[t][0] = sq[t][1] = 0.f;
   const bf16x8* W = p.W + (int64_t)cb * nkt * 64 + lane;
-  constexpr int NZ = 2 * G;  // 32-row chunks computed (rows past M are clamped copies, never stored)
+  // (rows past M are clamped copies, never stored)
   const int fr = lane & 15, fc = lane >> 4;  // fragment row within a 16-row block, 16-B chunk
   // Branch-free k loop (the compiler's own vmcnt bookkeeping then stays exact): the slice and weight
-  // prefetches are clamped to the last k-tile instead of skipped.  Issue order: W(0..5), S(0), W(6),
-  // S(1), W(7) | k-tile kt: S(kt+2), W(kt+8); so at the top of k-tile kt exactly W(kt+6), S(kt+1) and
-  // W(kt+7) -- G + 2 operations -- are younger than S(kt).  nkt % PD == 0 (host-checked).
+  // prefetches are clamped to the last k-tile instead of skipped.  Issue order: W(0 .. PD-LEAD-1), then
+  // S(i), W(PD-LEAD+i) for i < LEAD | k-tile kt: S(kt+LEAD), W(kt+PD); so at the top of k-tile kt exactly
+  // LEAD - 1 slices (G pieces each) and LEAD weight fragments are younger than S(kt), and W(kt) is older.
+  // nkt % PD == 0 (host-checked).  (NWV = 4: W(0..5), S(0), W(6), S(1), W(7); vmcnt(G + 2).)
+  constexpr int YOUNGER = G * (LEAD - 1) + LEAD;
   bf16x8 wr[PD];
 #pragma unroll
-  for (int u = 0; u < 6; ++u) wr[u] = __builtin_nontemporal_load(W + (int64_t)min(u, nkt - 1) * 64);
-  stage(0, 0);
-  wr[6] = __builtin_nontemporal_load(W + (int64_t)min(6, nkt - 1) * 64);
-  stage(1, min(1, nkt - 1));
-  wr[7] = __builtin_nontemporal_load(W + (int64_t)min(7, nkt - 1) * 64);
+  for (int u = 0; u < PD - LEAD; ++u) wr[u] = __builtin_nontemporal_load(W + (int64_t)min(u, nkt - 1) * 64);
+#pragma unroll
+  for (int i = 0; i < LEAD; ++i) {
+    stage(i, min(i, nkt - 1));
+    wr[PD - LEAD + i] = __builtin_nontemporal_load(W + (int64_t)min(PD - LEAD + i, nkt - 1) * 64);
+  }
   for (int kb = 0; kb < nkt; kb += PD) {
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
       const int kt = kb + u;
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(G + 2) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(YOUNGER) : "memory");
       lmr_barrier();
-      stage((kt + 2) % NBUF, min(kt + 2, nkt - 1));
+      stage((kt + LEAD) % NBUF, min(kt + LEAD, nkt - 1));
       const char* a = abuf[kt % NBUF];
       bf16x8 fa[2][2];
       auto rd = [&](int z, bf16x8 (&f)[2]) {
@@ -830,14 +838,14 @@ __global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
         }
         acc0[z] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[0], wr[u], acc0[z], 0, 0, 0);
         acc1[z] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f[1], wr[u], acc1[z], 0, 0, 0);
-        if ((z & 3) == wave) {
+        if (z % NWV == wave) {
 #pragma unroll
           for (int hh = 0; hh < 2; ++hh)
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               const float x = (float)f[hh][e];
-              ss[z >> 2][hh] += x;
-              sq[z >> 2][hh] = fmaf(x, x, sq[z >> 2][hh]);
+              ss[z / NWV][hh] += x;
+              sq[z / NWV][hh] = fmaf(x, x, sq[z / NWV][hh]);
             }
         }
       }
@@ -848,7 +856,7 @@ __global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
   // finish the statistics: the 4 lanes of a row (fc = 0..3) in chunk order
 #pragma unroll
   for (int t = 0; t < NSL; ++t) {
-    const int z = wave + 4 * t;
+    const int z = wave + NWV * t;
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       float a = ss[t][hh], b = sq[t][hh];
@@ -864,7 +872,7 @@ __global__ __launch_bounds__(256) void lm_head_rows_kernel(DecP p) {
   }
   __syncthreads();
   const int n = cb * 16 + fr;
-  if (blockIdx.x * 4 + wave >= n_cb || n >= p.N) return;
+  if (blockIdx.x * NWV + wave >= n_cb || n >= p.N) return;
   const float cs = p.ln_colsum[n], bn = p.bias ? p.bias[n] : 0.f;
   const float inv = 1.f / (float)p.K;
 #pragma unroll
@@ -1340,13 +1348,13 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     p.N = (int)a->N;
     p.K = (int)a->K;
     const int n_cb = (int)((a->N + 15) / 16);
-    const dim3 grid((unsigned)((n_cb + 3) / 4));
-    switch ((a->M + 63) / 64) {
-      case 1: hipLaunchKernelGGL(lm_head_rows_kernel<1>, grid, dim3(256), 0, s, p); break;
-      case 2: hipLaunchKernelGGL(lm_head_rows_kernel<2>, grid, dim3(256), 0, s, p); break;
-      case 3: hipLaunchKernelGGL(lm_head_rows_kernel<3>, grid, dim3(256), 0, s, p); break;
-      case 4: hipLaunchKernelGGL(lm_head_rows_kernel<4>, grid, dim3(256), 0, s, p); break;
-      default: hipLaunchKernelGGL(lm_head_rows_kernel<5>, grid, dim3(256), 0, s, p); break;
+    // eight 16-column waves per workgroup, four k-tile slices staged ahead (one workgroup per CU); a slice holds
+    // 128 G rows, G = ceil(M / 128)
+    const dim3 grid((unsigned)((n_cb + 7) / 8));
+    switch ((a->M + 127) / 128) {
+      case 1: hipLaunchKernelGGL((lm_head_rows_kernel<8, 1, 4>), grid, dim3(512), 0, s, p); break;
+      case 2: hipLaunchKernelGGL((lm_head_rows_kernel<8, 2, 8>), grid, dim3(512), 0, s, p); break;
+      default: hipLaunchKernelGGL((lm_head_rows_kernel<8, 3, LMR_NZ>), grid, dim3(512), 0, s, p); break;
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? KW_OK : kw_set_error(e);
