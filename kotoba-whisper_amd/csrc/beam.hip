@@ -385,19 +385,11 @@ __global__ __launch_bounds__(BT_S) void beam_logprobs_split_kernel(kw_beam_logpr
   // the slice's KP best processed scores (all tokens; and timestamps only, for the text-ban case):
   // each wave takes its own kp best by shuffle-only rounds (no workgroup barrier per round), then wave 0
   // takes the slice's kp best of the waves' 8 x kp
-#ifdef KW_BEAM_LAB_KP
-  const int kp = KW_BEAM_LAB_KP;  // lab: round count sweep (results wrong below K + 4)
-#else
   const int kp = min(K + 4, KP);
-#endif
   const int lane = tid & 63, wv = tid >> 6;
   __shared__ uint64_t wck[2][BT_S / 64][KP];
-#ifdef KW_BEAM_LAB_SKIP_TOPK
-  const int nlist = 0;  // lab: time the kernel without the slice top-k
-#else
   // timestamp tokens sit at the top of the vocabulary: only the slices holding some need the second list
   const int nlist = (st.rt && v1 > st.ts_begin) ? 2 : 1;
-#endif
   for (int list = 0; list < nlist; ++list) {
     // each lane keeps its 3 best keys below ``floor`` (the last key it gave up), refilled from its 16
     // registers in the rare round that empties it; a round is one wave max of the lanes' heads

@@ -26,7 +26,6 @@
 #include <stdlib.h>
 
 #include <algorithm>
-#include <array>
 
 #include "kw_common.h"
 
@@ -72,29 +71,10 @@ struct DecP {
   int zrows; // rows per grid z-chunk: 32, or 16 for narrow grids (row split, launch())
 };
 
-// The fused MLP's hand-off (dec_mlp_kernel below).  Producer (PUB, fc1): instead of storing its bf16 GELU tile to
-// C, a workgroup writes the tile to hx in the MFMA A-fragment layout fc2's waves load ([k-tile][row half][64 lanes]
-// [16 B]) by 16-B sc1 (write-through) stores, drains them and sets flags[cg] (MI355X_MICROARCH visibility table,
-// first row: sc1 stores, one lane's agent-scope flag, sc1 loads).  Consumer (CONS, fc2): a wave polls the flags of
-// its own k-tiles (two 16-column producers per k-tile), then loads their fragments by sc1 loads; the last consumer
-// workgroup through (done counter) re-arms the flags for the next launch.
-struct MlpPub {
-  char* hx;
-  int* flags;
-  int* fault;   // test hook: nonzero -> workgroup 0 skips its flag once (kw_dec_mlp_status_offset)
-  int* status;  // consumer: a poll timed out (its rows are NaN)
-  int* done;    // consumer workgroups past their polls
-  int n_cons, n_flags;
-};
-
 // H2: the second 16-row half of the tile exists (false: a row-split chunk of <= 16 rows -- its a1 / c1 / LayerNorm
 // statistics are never loaded or computed, which frees the registers for two workgroups per CU)
-// (mlp_wait: the consumer's flag poll, defined with the fused MLP below)
-__device__ __forceinline__ bool mlp_wait(const int* flags, int fidx, int lane, int* status);
-
-template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool PUB, bool H2 = true, bool CONS = false>
-__device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int cg, const int ks, const int nw,
-                                                const MlpPub& pub) {
+template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool H2 = true>
+__device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int cg, const int ks, const int nw) {
   __shared__ f32x4 red[MAXW][NCB][2][64];
   __shared__ float rpart[MAXW][32][2];  // LayerNorm: per-wave row (sum, sum of squares)
   __shared__ float rstat[32][2];     // LayerNorm: (mean, rstd) per row
@@ -127,7 +107,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     }
   const int wkt0 = (nkt * ks) / ksn, wkt1 = (nkt * (ks + 1)) / ksn;  // this workgroup's k-tiles
   const int cpr = (wkt1 - wkt0) * 4, cprp = cpr + 1;
-  const bool xlds = !CONS && p.xlds;
+  const bool xlds = p.xlds;
   if (xlds) {
     // <= 16 rows: only the pieces of rows 0..15 (the second row half's fragments then hold stale LDS, and its
     // output rows -- all >= M -- are discarded; every row of an MFMA tile is independent of the others)
@@ -171,35 +151,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     }
   }
 
-  if constexpr (CONS) {
-    // the producers' fragments of this wave's k-tiles: one poll over their flags (lane l: flag 2 kt0 + l), then sc1
-    // loads (written in this launch by other CUs); a poll that timed out turns the operands into NaN
-    const int fidx = lane < 2 * (kt1 - kt0) ? 2 * kt0 + lane : -1;
-#if defined(KW_MLP_LAB) && (KW_MLP_LAB == 1 || KW_MLP_LAB == 3)
-    const bool ok = fidx >= -1;  // lab decomposition: no wait (results wrong, timing real)
-#else
-    const bool ok = mlp_wait(pub.flags, fidx, lane, pub.status);
-#endif
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (no instruction: keeps the loads below the poll)
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx, (short)0, nkt * 2048, 0x00020000);
-#pragma unroll
-    for (int u = 0; u < KTM; ++u) {
-      const int kt = min(kt0 + u, ktl);
-      a0[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 0) * 1024 + lane * 16, 0, 16));
-      if constexpr (H2)
-        a1[u] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(rs, (kt * 2 + 1) * 1024 + lane * 16, 0, 16));
-    }
-    if (!ok) {
-      bf16x8 nan;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) nan[e] = (__bf16)__builtin_nanf("");
-#pragma unroll
-      for (int u = 0; u < KTM; ++u) {
-        a0[u] = nan;
-        a1[u] = nan;
-      }
-    }
-  } else if (xlds) {
+  if (xlds) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 #pragma unroll
@@ -279,14 +231,6 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     }
     __syncthreads();
     if (wave != 0) return;
-    if constexpr (CONS) {  // every wave of this workgroup is past its polls: the last consumer re-arms the flags
-      int last = 0;
-      if (lane == 0) last = __hip_atomic_fetch_add(pub.done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == pub.n_cons - 1;
-      if (__shfl(last, 0, 64)) {
-        for (int i = lane; i < pub.n_flags; i += 64) __hip_atomic_store(pub.flags + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (lane == 0) __hip_atomic_store(pub.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    }
     for (int w2 = 1; w2 < nw; ++w2)
 #pragma unroll
       for (int c = 0; c < NCB; ++c) {
@@ -381,43 +325,9 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
         } else {
           if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
           if (n < p.scale_cols) v *= p.scale;
-          if constexpr (PUB) {
-            // every row (rows >= M are clamped copies: fc2 discards them), row-major 32 x 16 NCB tile in LDS
-            reinterpret_cast<bf16_t*>(xs)[m * (16 * NCB + 8) + c * 16 + (lane & 15)] = f2bf(v);
-          } else {
-            if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
-          }
+          if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
         }
       }
-    }
-  }
-  if constexpr (PUB) {
-    // wave 0 alone: the tile back out in fragment order (row 16 hh + lane % 16, columns 8 (lane / 16) + 0..7),
-    // two 16-B write-through stores per lane, drained, then one lane sets this k-tile's flag
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if constexpr (NCB == 2) {  // 32 columns = fc2's k-tile cg
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx + (int64_t)cg * 2048, (short)0, 2048, 0x00020000);
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const u32x4 t = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(xs) + (16 * hh + (lane & 15)) * 40 +
-                                                        8 * (lane >> 4));
-        __builtin_amdgcn_raw_buffer_store_b128(t, rs, (hh * 64 + lane) * 16, 0, 16);  // aux 16 = sc1
-      }
-    } else {  // 16 columns = half q = cg & 1 of k-tile cg >> 1: fragment lanes r + 16 (2 q + j), one 16-B piece per lane
-      const int hh = lane >> 5, r = lane & 15, j = (lane >> 4) & 1;
-      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(pub.hx + (int64_t)(cg >> 1) * 2048, (short)0, 2048, 0x00020000);
-      const u32x4 t = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(xs) + (16 * hh + r) * 24 + 8 * j);
-      __builtin_amdgcn_raw_buffer_store_b128(t, rs, (hh * 64 + r + 16 * (2 * (cg & 1) + j)) * 16, 0, 16);
-    }
-    const int fault = __hip_atomic_load(pub.fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (lane == 0) {
-      if (cg == 0 && fault != 0)
-        __hip_atomic_store(pub.fault, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // drop this launch's flag once
-      else
-        __hip_atomic_store(pub.flags + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   KW_DEC_STAMP(4);
@@ -443,66 +353,8 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
   } else {
     p.M = min(p0.zrows, p0.M);
   }
-  dec_linear_body<KTM, NCB, LNA, EPI, TC, false, H2>(p, ksn, blockIdx.x, blockIdx.y, blockDim.x >> 6, MlpPub{});
+  dec_linear_body<KTM, NCB, LNA, EPI, TC, H2>(p, ksn, blockIdx.x, blockIdx.y, blockDim.x >> 6);
 }
-
-#ifdef KW_LAB_MLP
-// ---- fused decode MLP: fc1 (LayerNorm-fused, GELU) -> fc2 (+ residual) in ONE launch (kw_dec_mlp) ----
-// LAB ONLY (make EXTRA=-DKW_LAB_MLP; tools/lab/mlp_coresident.py): it lost to the two kw_dec_linear launches (r04's
-// fc2-concentrated design 19.8 vs 18.6 us; this co-resident one 22.4-23.3, profiles/r05b_mlp_decomposition.txt), so
-// libkwhisper.so does not carry it.
-// r05, co-resident roles: workgroups [0, n1) are fc1, one per 16 columns (dec_linear_body<5, 1,
-// LN, STORE, GELU>: 8 waves x 5 k-tiles, each activation fragment loaded straight from hb -- no LDS image, so the
-// launch needs no more LDS than its reduction buffers), each publishing its tile -- half of one of fc2's k-tiles --
-// through MlpPub; workgroups [n1, n1 + n2) are fc2's split-K grid (one per (16 columns, K-split): 8 waves x 5 k-tiles,
-// the deterministic seam of the split-K launch), every one of them spread over the CUs beside fc1 and streaming its
-// weights while fc1 runs; a wave waits only for the flags of its own k-tiles.  r04's version gave fc2 80 workgroups
-// of all the K-splits each: it read the whole activation per workgroup and lost (19.8 vs 18.6 us).  Every wait is on
-// a workgroup dispatched earlier in the same launch (fc1 never waits), so the launch cannot deadlock at any
-// residency; a poll that outlasts MLP_SPIN_LIMIT sets the status word and writes NaN rows
-// (kw_dec_mlp_status_offset).  fc1's values are bitwise those of its own launch (the same per-element arithmetic);
-// fc2 sums its K in 5-k-tile slices, 4 K-splits (f32 summation order of its own).
-constexpr int MLP_HDR = 1024;            // workspace ints before the fragment image: flags, done, status, fault
-constexpr int MLP_DONE = MLP_HDR - 4, MLP_STATUS = MLP_HDR - 3, MLP_FAULT = MLP_HDR - 2;
-constexpr int MLP_SPIN_LIMIT = 1 << 22;
-constexpr int MLP_CNT = 1024;            // fc2 seam counters (one per column block)
-
-struct MlpArgs {
-  DecP f1, f2;  // fc1: LayerNorm-fused STORE (gelu, bf16, no LDS image); fc2: RESID (h, hb), split-K seam
-  MlpPub pub;
-  int n1;       // fc1 workgroups (= F / 16)
-  int ncb2, ks2;  // fc2 column blocks and K-splits (n2 = ncb2 * ks2 workgroups)
-};
-
-// One wave polls up to 64 flags at once: lane l the flag fidx (< 0: none).
-__device__ __forceinline__ bool mlp_wait(const int* flags, int fidx, int lane, int* status) {
-  const bool mine = fidx >= 0;
-  const int* f = flags + (mine ? fidx : 0);
-  for (int it = 0;; ++it) {
-    const int v = __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (__builtin_amdgcn_ballot_w64(mine && v == 0) == 0) return true;
-    if (it >= MLP_SPIN_LIMIT) {
-      if (lane == 0) __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(KW_POLL_SLEEP);
-  }
-}
-
-__global__ __launch_bounds__(512) void dec_mlp_kernel(MlpArgs a) {
-#if defined(KW_MLP_LAB) && KW_MLP_LAB == 2
-  if ((int)blockIdx.x >= a.n1) return;  // lab decomposition: the fc1 role alone
-#elif defined(KW_MLP_LAB) && KW_MLP_LAB == 3
-  if ((int)blockIdx.x < a.n1) return;  // lab decomposition: the fc2 role alone (no waits)
-#endif
-  if ((int)blockIdx.x < a.n1) {
-    dec_linear_body<5, 1, true, KW_EPI_STORE, bf16_t, true>(a.f1, 1, blockIdx.x, 0, 8, a.pub);
-  } else {
-    const int j = blockIdx.x - a.n1;
-    dec_linear_body<5, 1, false, KW_EPI_RESID, float, false, true, true>(a.f2, a.ks2, j % a.ncb2, j / a.ncb2, 8, a.pub);
-  }
-}
-#endif  // KW_LAB_MLP
 
 // More than 32 rows without a K split (prefill positions, beam rows): each workgroup keeps its
 // columns' weight fragments in registers and walks ``zper`` 32-row chunks.  (One z-slice per chunk
@@ -902,16 +754,12 @@ __global__ __launch_bounds__(64 * NWV) void lm_head_rows_kernel(DecP p) {
 // epilogue load in the loop), each prefetch is pinned where it is written (sched_barrier: the scheduler had sunk
 // the next group's loads below the current group's waits), and the per-group barrier is a raw s_barrier after an
 // LDS-only wait (__syncthreads drained every load in flight, the prefetch included).
-#ifndef KW_LMH_MAX_ROWS
-#define KW_LMH_MAX_ROWS 32  // (lab knob: rows up to which the LM head takes lm_head_kernel)
-#endif
 constexpr int LMH_KTM = 5;   // k-tiles per wave
 constexpr int LMH_NCB = 2;   // column blocks per group
 constexpr int LMH_MAXG = 8;  // column groups per workgroup (epilogue constants and the logits staged in LDS; host-checked)
 constexpr int LMH_ECJ = 4;   // epilogue-constant columns staged per thread (host-checked: 64 * waves * 4 >= 32 * groups)
-#ifndef KW_LMH_BUFS
-#define KW_LMH_BUFS 3  // weight groups in registers: two in flight beside the one being multiplied (2: one)
-#endif
+constexpr int LMH_MAX_ROWS = 32;  // rows up to which the LM head takes lm_head_kernel (weight groups: three in
+                                  // registers, two in flight beside the one being multiplied)
 
 __device__ __forceinline__ void lmh_barrier() {  // LDS writes visible, then s_barrier: global loads stay in flight
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -975,10 +823,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       a1[u] = *reinterpret_cast<const bf16x8*>(p.x + (int64_t)r1 * p.ldx + k);
     }
   }
-  bf16x8 wa[LMH_NCB][LMH_KTM], wb[LMH_NCB][LMH_KTM];
-#if KW_LMH_BUFS == 3
-  bf16x8 wc[LMH_NCB][LMH_KTM];
-#endif
+  bf16x8 wa[LMH_NCB][LMH_KTM], wb[LMH_NCB][LMH_KTM], wc[LMH_NCB][LMH_KTM];
   wload(g0, wa);
   wload(g0 + 1, wb);
 #pragma unroll
@@ -1040,15 +885,6 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
     __syncthreads();
   }
   // walk the run: groups g+1 and g+2 in flight while group g is multiplied, reduced and stored
-#if defined(KW_LMH_LAB) && KW_LMH_LAB == 2
-  uint32_t sink = 0;  // lab decomposition: the weight stream alone (no MFMA, barrier or epilogue)
-  auto body = [&](int g, int slot, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
-#pragma unroll
-    for (int c = 0; c < LMH_NCB; ++c)
-#pragma unroll
-      for (int u = 0; u < LMH_KTM; ++u) sink ^= __builtin_bit_cast(u32x4, w[c][u])[0];
-  };
-#else
   auto body = [&](int g, int slot, bf16x8 (&w)[LMH_NCB][LMH_KTM]) {
     f32x4 c0[LMH_NCB], c1[LMH_NCB];
 #pragma unroll
@@ -1083,8 +919,6 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       }
     }
   };
-#endif
-#if KW_LMH_BUFS == 3
   int g = g0;
   for (; g + 2 < g1; g += 3) {
     wload(g + 2, wc);
@@ -1096,19 +930,6 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   }
   if (g < g1) body(g, 0, wa);
   if (g + 1 < g1) body(g + 1, 1, wb);
-#if defined(KW_LMH_LAB) && KW_LMH_LAB == 2
-  if (sink == 0x12345678u) reinterpret_cast<float*>(p.C)[tid] = 0.f;
-#endif
-#else
-  for (int g = g0 + 1; g < g1; g += 2) {  // (group g0 + 1 is already in flight)
-    body(g - 1, 0, wa);
-    wload(g + 1, wa);
-    body(g, 1, wb);
-    wload(g + 2, wb);
-  }
-  if ((g1 - g0) & 1) body(g1 - 1, 0, wa);
-#endif
-#if !defined(KW_LMH_LAB) || KW_LMH_LAB != 2
   // the run's logits: row m's columns [32 g0, 32 g1) as one contiguous span (each wave instruction 64 consecutive
   // floats = 256 B), non-temporal
   lmh_barrier();
@@ -1116,12 +937,8 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   float* cbase = reinterpret_cast<float*>(p.C) + g0 * LMH_NCB * 16;
   for (int i = tid; i < M * ncol; i += blockDim.x) {
     const int m = i / ncol, col = i - m * ncol;
-#if defined(KW_LMH_LAB) && KW_LMH_LAB == 1
-    if (obuf[m][col] == 1234.5678f)  // lab decomposition: no logit stores (timing real, results wrong)
-#endif
     __builtin_nontemporal_store(obuf[m][col], cbase + (int64_t)m * p.ldc + col);
   }
-#endif
 }
 
 __global__ void pack_kernel(const bf16_t* __restrict__ W, int N, int K, bf16_t* __restrict__ out) {
@@ -1167,24 +984,6 @@ Geo choose(int64_t N, int64_t K) {
   // r04: the split fc2 (6 x 27 k-tiles) on 6 waves of 5 k-tiles instead of 3 of 10 -- more loads in flight per
   // workgroup: 9.79-9.89 vs 10.27-10.29 us (profiles/r04c_splitk_sweep.txt; ks 8 / 4 and the o-proj split worse)
   if (g.ks > 1 && per_wg0 <= 5 * MAXW && N < 8192) g.ktm = 5;
-#ifdef KW_LAB_OVERRIDES
-  // lab builds only (make EXTRA=-DKW_LAB_OVERRIDES OUT=...; tools/lab/*_sweep.sh): KW_DECLIN_GEO="N,K,ncb,ktm,ks"
-  // overrides one matrix shape's geometry; read once, thread-safe (function-local static)
-  static const std::array<int, 5> lab = [] {
-    std::array<int, 5> v{0, 0, 0, 0, 0};
-    if (const char* e = getenv("KW_DECLIN_GEO")) {
-      sscanf(e, "%d,%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3], &v[4]);
-      fprintf(stderr, "kwhisper: lab geometry override KW_DECLIN_GEO=%s\n", e);
-    }
-    return v;
-  }();
-  if (lab[0] == N && lab[1] == K && (lab[2] == 1 || lab[2] == 2) && (lab[3] == 5 || lab[3] == 10) && lab[4] >= 1 &&
-      lab[4] <= KSMAX) {
-    g.ncb = lab[2];
-    g.ktm = lab[3];
-    g.ks = lab[4];
-  }
-#endif
   const int per_wg = (nkt + g.ks - 1) / g.ks;
   g.nw = (per_wg + g.ktm - 1) / g.ktm;
   if (g.nw > MAXW) {  // very long K: more splits
@@ -1204,18 +1003,6 @@ size_t x_lds_bytes_for(int nkt, int ks, bool xlds) { return xlds ? x_lds_bytes((
 // the image of a <= 16-row chunk (row split): only its rows' pieces are staged
 size_t x_lds_bytes_rows(int tiles, int rows, bool xlds) {
   return xlds ? (size_t)((rows * (4 * tiles + 1) + 63) / 64) * 1024 : 0;
-}
-
-bool row_split_on() {
-#ifdef KW_LAB_OVERRIDES
-  static const bool on = [] {  // lab builds: KW_DECLIN_ROWSPLIT=0 turns the row split off (A/B)
-    const char* e = getenv("KW_DECLIN_ROWSPLIT");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-#else
-  return true;
-#endif
 }
 
 int device_cus() {
@@ -1259,7 +1046,7 @@ hipError_t launch_one(const DecP& p, const Geo& g, hipStream_t s) {
   // bitwise the 32-row launch.  o 5.05 -> 4.13-4.29 us; fc1 (160 -> 320 workgroups, two per CU) measured
   // 8.6 -> 8.7-8.9 us, so it keeps one launch of 32-row tiles (profiles/r04o_rowsplit_ab.txt)
   const int ncg = (p.N + 16 * NCB - 1) / (16 * NCB);
-  const bool split = g.ks == 1 && p.M > 16 && p.M <= 32 && 2 * ncg <= device_cus() && row_split_on();
+  const bool split = g.ks == 1 && p.M > 16 && p.M <= 32 && 2 * ncg <= device_cus();
   DecP q = p;
   q.zrows = split ? 16 : 32;
   const dim3 grid((unsigned)ncg, (unsigned)g.ks, (unsigned)((p.M + q.zrows - 1) / q.zrows));
@@ -1333,7 +1120,7 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
   // 32 rows, the all-rows GEMM up to LMR_MAXROWS (beam rows), the weight-stationary rows kernel beyond
   const bool lm_shape = a->ln && a->epilogue == KW_EPI_STORE && a->c_dtype == KW_DT_F32 && a->N >= 8192 && !a->gelu &&
                         a->scale_cols == 0;
-  if (lm_shape && a->M > KW_LMH_MAX_ROWS && a->M <= LMR_MAXROWS && nkt % 8 == 0) {
+  if (lm_shape && a->M > LMH_MAX_ROWS && a->M <= LMR_MAXROWS && nkt % 8 == 0) {
     DecP p{};
     p.x = reinterpret_cast<const bf16_t*>(a->x);
     p.ldx = a->ldx;
@@ -1359,7 +1146,7 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? KW_OK : kw_set_error(e);
   }
-  const bool lmh = lm_shape && (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && a->M <= KW_LMH_MAX_ROWS &&
+  const bool lmh = lm_shape && (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && a->M <= LMH_MAX_ROWS &&
                    lmh_groups_per_wg(a->N) <= LMH_MAXG &&
                    64 * ((nkt + LMH_KTM - 1) / LMH_KTM) * LMH_ECJ >= lmh_groups_per_wg(a->N) * LMH_NCB * 16;
   // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each)
@@ -1414,97 +1201,3 @@ extern "C" int kw_pack_weight(const void* W, int64_t N, int64_t K, void* packed,
   KW_CHECK_LAUNCH();
   return KW_OK;
 }
-
-#ifdef KW_LAB_MLP
-#include "../../tools/lab/kw_mlp_lab.h"
-
-// ---- kw_dec_mlp (dec_mlp_kernel): fc1 -> fc2 of a greedy decode step in one launch ----
-namespace {
-
-// fc1: 16-column workgroups of 8 waves x <= 5 k-tiles (K = d <= 1280); fc2: K-splits of 8 waves x 5 k-tiles
-// (ks2 = F / 1280 at large-v3), <= KSMAX splits
-bool mlp_geometry(int64_t M, int64_t d, int64_t F, int& ks2) {
-  if (M < 1 || M > 32 || d <= 0 || F <= 0 || d % 32 != 0 || F % 32 != 0) return false;
-  const int nkt1 = (int)(d / 32), nkt2 = (int)(F / 32);
-  if (nkt1 > 8 * 5 || F / 16 > MLP_DONE || d / 16 > MLP_CNT) return false;
-  ks2 = (nkt2 + 39) / 40;
-  return ks2 <= KSMAX && (nkt2 + ks2 * 8 - 1) / (ks2 * 8) <= 5;
-}
-
-size_t mlp_hx_bytes(int64_t F) { return (size_t)(F / 32) * 2048; }
-
-}  // namespace
-
-extern "C" int kw_dec_mlp_supported(int64_t M, int64_t d, int64_t F) {
-  int ks2;
-  return mlp_geometry(M, d, F, ks2) ? 1 : 0;
-}
-
-extern "C" size_t kw_dec_mlp_workspace(int64_t M, int64_t d, int64_t F) {
-  (void)M;
-  int ks2 = 1;
-  mlp_geometry(1, d, F, ks2);
-  return (size_t)MLP_HDR * sizeof(int) + mlp_hx_bytes(F) + (size_t)MLP_CNT * sizeof(int) +
-         (size_t)((d + 15) / 16) * ks2 * 512 * sizeof(float);
-}
-
-extern "C" size_t kw_dec_mlp_status_offset(int64_t M, int64_t d, int64_t F) {
-  (void)M;
-  (void)d;
-  (void)F;
-  return (size_t)MLP_STATUS * sizeof(int);
-}
-
-extern "C" int kw_dec_mlp(const kw_dec_mlp_args* a, kw_stream_t stream) {
-  if (!a || !a->x || !a->fc1_w || !a->fc1_colsum || !a->fc2_w || !a->h || !a->hb || !a->workspace)
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_mlp: null pointer");
-  int ks2;
-  if (!mlp_geometry(a->M, a->d, a->F, ks2))
-    return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_mlp: shape not covered (kw_dec_mlp_supported)");
-  if (a->ldx < a->d || a->ldx % 8 != 0 || (uintptr_t)a->x % 16 != 0 || a->ldh < a->d)
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_mlp: ldx >= d (multiple of 8, x 16-B aligned), ldh >= d");
-  if (a->ws_bytes < kw_dec_mlp_workspace(a->M, a->d, a->F) || (uintptr_t)a->workspace % 16 != 0)
-    return kw_set_error_msg(KW_EINVAL, "kw_dec_mlp: needs a zero-filled, 16-B aligned workspace of kw_dec_mlp_workspace()");
-  MlpArgs m{};
-  DecP& p1 = m.f1;
-  p1.x = reinterpret_cast<const bf16_t*>(a->x);
-  p1.ldx = a->ldx;
-  p1.ln = 1;
-  p1.ln_eps = a->ln_eps;
-  p1.ln_colsum = a->fc1_colsum;
-  p1.W = reinterpret_cast<const bf16x8*>(a->fc1_w);
-  p1.bias = a->fc1_bias;
-  p1.gelu = 1;
-  p1.scale = 1.f;
-  p1.scale_cols = 0;
-  p1.M = (int)a->M;
-  p1.N = (int)a->F;
-  p1.K = (int)a->d;
-  p1.xlds = 0;
-  p1.zrows = 32;
-  char* ws = reinterpret_cast<char*>(a->workspace);
-  DecP& p2 = m.f2;
-  p2.W = reinterpret_cast<const bf16x8*>(a->fc2_w);
-  p2.bias = a->fc2_bias;
-  p2.h = a->h;
-  p2.hb = reinterpret_cast<bf16_t*>(a->hb);
-  p2.ldh = a->ldh;
-  p2.M = (int)a->M;
-  p2.N = (int)a->d;
-  p2.K = (int)a->F;
-  p2.xlds = 0;
-  p2.zrows = 32;
-  p2.cnt = reinterpret_cast<int*>(ws + MLP_HDR * sizeof(int) + mlp_hx_bytes(a->F));
-  p2.slab = reinterpret_cast<float*>(reinterpret_cast<char*>(p2.cnt) + MLP_CNT * sizeof(int));
-  int* hdr = reinterpret_cast<int*>(ws);
-  m.n1 = (int)(a->F / 16);
-  m.ncb2 = (int)((a->d + 15) / 16);
-  m.ks2 = ks2;
-  m.pub = MlpPub{ws + MLP_HDR * sizeof(int), hdr, hdr + MLP_FAULT, hdr + MLP_STATUS, hdr + MLP_DONE, m.ncb2 * ks2, m.n1};
-  const size_t shm = 32 * 24 * sizeof(bf16_t);  // the producer's 32 x 16 tile (row stride 24)
-  const unsigned grid = (unsigned)(m.n1 + m.ncb2 * ks2);
-  hipLaunchKernelGGL(dec_mlp_kernel, dim3(grid), dim3(512), shm, (hipStream_t)stream, m);
-  const hipError_t e = hipGetLastError();
-  return e == hipSuccess ? KW_OK : kw_set_error(e);
-}
-#endif  // KW_LAB_MLP

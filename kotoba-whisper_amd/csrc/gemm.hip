@@ -514,14 +514,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
             *c = o;
           } else {
             if (p.gelu) {
-#if defined(KW_GEMM_LAB) && KW_GEMM_LAB == 1
-#pragma unroll
-              for (int e = 0; e < VEC; ++e) v[e] = (v[e] + cadd[e]) * cmul[e];  // lab: the epilogue without GELU
-#else
 #pragma unroll
               for (int e = 0; e < VEC; ++e)
                 v[e] = (sizeof(TC) == 2 ? gelu_bf16out(v[e] + cadd[e]) : gelu_erf(v[e] + cadd[e])) * cmul[e];
-#endif
             } else {
 #pragma unroll
               for (int e = 0; e < VEC; ++e) v[e] = fmaf(v[e], cmul[e], cadd[e]);
@@ -548,9 +543,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmP p) {
               // the out-proj / fc2 deltas stay cacheable for the HBM-bound LayerNorm that reads them next
               const bool nt = EPI == KW_EPI_HEADSPLIT || p.gelu;
               typedef __attribute__((ext_vector_type(4))) unsigned int nt_u4;
-#if defined(KW_GEMM_LAB) && KW_GEMM_LAB == 2
-              if (o.x == 0x12345678u)  // lab: the epilogue without its stores (timing real, results wrong)
-#endif
               if (nt)
                 __builtin_nontemporal_store(nt_u4{o.x, o.y, o.z, o.w}, reinterpret_cast<nt_u4*>(reinterpret_cast<bf16_t*>(p.C) + off));
               else
@@ -665,23 +657,14 @@ hipError_t launch256(const GemmP& p, int epi, hipStream_t s) {
   }
 }
 
-// 256x256 ping-pong for the big GEMMs; KW_GEMM_TILE=128 (env) forces the 128x128 kernel (A/B runs).
+// 256x256 ping-pong for the big GEMMs (the 128x128 kernel for shapes it does not take).
 bool use256(const kw_gemm_args* a) {
-#ifdef KW_LAB_OVERRIDES
-  // lab builds only: KW_GEMM_TILE=128 forces the 128x128 kernel (tools/gemm_bench.py)
-  static const int forced = [] {
-    const char* e = getenv("KW_GEMM_TILE");
-    return (e && atoi(e) == 128) ? 1 : 0;
-  }();
-#else
-  constexpr int forced = 0;
-#endif
   // vector epilogue: ldc, batch strides, head_dim in whole 16-B pieces, the C base 16-B aligned
   const int vec = (a->c_dtype == KW_DT_F32) ? 4 : 8;  // 16-B pieces: 4 f32 / 8 bf16 columns
   const bool aligned = a->ldc % vec == 0 && a->c_batch_stride % vec == 0 &&
                        (a->hs_head_dim <= 0 || a->hs_head_dim % vec == 0) && ((uintptr_t)a->C % 16) == 0 &&
                        ((uintptr_t)a->row_add % 16) == 0;
-  return !forced && aligned && a->N % PB == 0 && a->M >= 4 * PB;
+  return aligned && a->N % PB == 0 && a->M >= 4 * PB;
 }
 
 template <typename TC>

@@ -59,8 +59,11 @@ __global__ __launch_bounds__(THREADS) void logmel_kernel(const float* __restrict
     double a = 6.283185307179586476925 * (double)i / N_FFT;
     win[i] = (double)(float)(0.5 - 0.5 * cos(a));  // torch.hann_window(400) (periodic), f32 values
   }
-  // each mel filter's nonzero bins: the projection below sums only those, in the same bin order -- bitwise the
-  // dense sum (a zero weight adds +0 to the f32 accumulator) at a fraction of its 201 multiply-adds per output
+  // each mel filter's nonzero bins: the projection below sums only those, in the same bin order -- for FINITE power
+  // spectra bitwise the dense sum (a zero weight adds +0 to the f32 accumulator) at a fraction of its 201
+  // multiply-adds per output.  Non-finite audio differs: the dense sum's 0 * Inf terms make every mel bin NaN (as
+  // the reference's mel_filters.T @ magnitudes does), the sparse sum keeps bins whose filter range avoids the bad
+  // frequency bins finite (parity on non-finite input is unpinned)
   for (int m = tid; m < n_mels; m += THREADS) {
     int lo = N_BINS, hi = 0;
     for (int k0 = 0; k0 < N_BINS; k0 += 8) {

@@ -212,7 +212,9 @@ def check(rc: int, what: str) -> None:
 
 _OWN_STREAMS = []  # (raw handle, torch stream): every stream made here, kept for the process's lifetime
 _FREE_STREAMS = {}  # device index -> streams whose owner is gone, handed out again before a new one is made
-_STREAM_LOCK = threading.Lock()
+# re-entrant: release_stream also runs from weakref.finalize callbacks, i.e. from whatever allocation on this thread
+# triggers a garbage collection -- possibly inside new_stream's own locked section
+_STREAM_LOCK = threading.RLock()
 
 
 def new_stream(device=None, owner=None):
@@ -228,16 +230,17 @@ def new_stream(device=None, owner=None):
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     if dev.index is None:  # "cuda": the current device (free lists are keyed by index, as s.device.index)
         dev = torch.device("cuda", torch.cuda.current_device())
+    free = _FREE_STREAMS.setdefault(dev.index, [])  # (allocation outside the lock; setdefault is atomic)
     with _STREAM_LOCK:
-        free = _FREE_STREAMS.setdefault(dev.index, [])
         s = free.pop() if free else None
     if s is None:
         h = ctypes.c_void_p()
         with torch.cuda.device(dev):
             check(load().kw_stream_create(ctypes.byref(h)), "kw_stream_create")
         s = torch.cuda.ExternalStream(h.value, device=dev)
+        entry = (h, s)
         with _STREAM_LOCK:
-            _OWN_STREAMS.append((h, s))
+            _OWN_STREAMS.append(entry)
     if owner is not None:
         weakref.finalize(owner, release_stream, s)
     return s
@@ -246,5 +249,6 @@ def new_stream(device=None, owner=None):
 def release_stream(s) -> None:
     """Hand a ``new_stream`` stream back (its owner is done with it; work already queued on it stays ordered ahead of
     whatever its next user queues)."""
+    free = _FREE_STREAMS.setdefault(s.device.index, [])
     with _STREAM_LOCK:
-        _FREE_STREAMS.setdefault(s.device.index, []).append(s)
+        free.append(s)

@@ -112,3 +112,16 @@ def test_torch_ops_reject_host_tensors(lib):
     kw = _lib.load_torch_ops()
     with pytest.raises((ValueError, NotImplementedError)):
         kw.attention(torch.zeros(3 * 64), 1, 1, 1, 64, torch.zeros(64))
+
+
+def test_integration_doc_names_only_declared_symbols():
+    """every ``kw_*`` entry point INTEGRATION.md names (its ABI table, the ctypes stub) is one the
+    header declares -- so a symbol that leaves the library cannot linger in the maintainer's guide.  Struct and type
+    names (kw_*_args, kw_stream_t) are not entry points."""
+    doc = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    named = {n for n in re.findall(r"\b(kw_[a-z0-9_]+)\b", doc) if not n.endswith(("_args", "_t"))}
+    # "`kw_dec_qkv_self` (+ `_workspace`, `_supported`)": the suffixes name kw_dec_qkv_self_workspace etc.
+    for base, rest in re.findall(r"`(kw_[a-z0-9_]+)` \(\+ ([^)]*)\)", doc):
+        named |= {base + s for s in re.findall(r"`(_[a-z0-9_]+)`", rest)}
+    missing = sorted(named - set(_declared()))
+    assert named and not missing, missing

@@ -284,7 +284,7 @@ def test_pipeline_data_parallel_gloo_matches_single_process(tmp_path, world):
     assert sum(calls) == m1.calls and max(calls) - min(calls) <= 1
 
 
-def _dp_mismatch_worker(rank, world, port, out_dir):
+def _dp_mismatch_worker(rank, world, port, out_dir, mode="reversed"):
     import torch.distributed as dist
 
     from kwhisper.pipeline import ASRPipeline
@@ -292,8 +292,19 @@ def _dp_mismatch_worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         clips = _dp_clips()
-        if rank == 1:  # a per-rank shard of the inputs: another clip in position 2 (same window count)
+        if rank == 1 and mode == "reversed":  # a per-rank shard of the inputs: another clip in position 2 (same window count)
             clips[2] = {"array": clips[2]["array"][::-1].copy(), "sampling_rate": 16000}
+        elif rank == 1:  # the same edges (silent start and end), different audio in the middle of a window
+            for c in clips:
+                c["array"][:4000] = 0.0
+                c["array"][-4000:] = 0.0
+            a = clips[1]["array"].copy()
+            a[len(a) // 2] += 0.25
+            clips[1] = {"array": a, "sampling_rate": 16000}
+        if mode == "middle" and rank == 0:
+            for c in clips:
+                c["array"][:4000] = 0.0
+                c["array"][-4000:] = 0.0
         msg, m = "", _StubASRModel()
         try:
             ASRPipeline(m, feature_extractor=_StubFE(), chunk_length_s=15, batch_size=2, data_parallel=True)(clips)
@@ -307,9 +318,12 @@ def _dp_mismatch_worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-def test_pipeline_data_parallel_refuses_different_inputs(tmp_path):
+@pytest.mark.parametrize("mode", ["reversed", "middle"])
+def test_pipeline_data_parallel_refuses_different_inputs(tmp_path, mode):
     """data_parallel is opt-in, and with it every rank must pass the same inputs -- ranks holding
-    different audio raise ValueError on every rank (before any window batch is split or gathered)."""
+    different audio raise ValueError on every rank (before any window batch is split or gathered).  ADVICE r05
+    ("middle"): the ranks' clips share silent starts and ends and differ in one sample in the middle of a window,
+    which a digest of the window edges alone would miss."""
     import socket
 
     import torch.multiprocessing as mp
@@ -317,7 +331,7 @@ def test_pipeline_data_parallel_refuses_different_inputs(tmp_path):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.spawn(_dp_mismatch_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    mp.spawn(_dp_mismatch_worker, args=(2, port, str(tmp_path), mode), nprocs=2, join=True)
     for r in range(2):
         assert "same inputs on every rank" in open(tmp_path / f"m{r}.txt").read()
 

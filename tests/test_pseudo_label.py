@@ -468,19 +468,41 @@ class _SlowModel(_CountingModel):
     """Batches holding an item of ``slow`` take ``delay`` seconds (a batch with extra seek passes); ``"first"`` in
     ``slow`` makes the model's first batch slow, whichever batch its rank claimed first."""
 
-    def __init__(self, slow=(), delay=0.0):
+    def __init__(self, slow=(), delay=0.0, wait_for=None, report=None, announce=None):
         super().__init__()
         self.first = "first" in slow
         self.slow, self.delay = {s for s in slow if s != "first"}, delay
         self.calls = 0
+        self.wait_for, self.report = wait_for, report  # (path, count): first call blocks until path holds >= count
+        self.announce = announce  # a file the first call writes "1" into before anything else
 
     def generate(self, feats, **kw):
         import time
 
         self.calls += 1
-        if (self.first and self.calls == 1) or self.slow & set(feats[:, 0].long().tolist()):
+        if self.announce is not None and self.calls == 1:
+            with open(self.announce + ".tmp", "w") as f:
+                f.write("1")
+            os.replace(self.announce + ".tmp", self.announce)
+        if self.wait_for is not None and self.calls == 1:
+            path, count = self.wait_for
+            t_end = time.time() + 60.0  # bounded: a failure, not a hang
+            while time.time() < t_end:
+                try:
+                    if int(open(path).read() or 0) >= count:
+                        break
+                except (OSError, ValueError):
+                    pass
+                time.sleep(0.01)
+        elif (self.first and self.calls == 1) or self.slow & set(feats[:, 0].long().tolist()):
             time.sleep(self.delay)
-        return super().generate(feats, **kw)
+        out = super().generate(feats, **kw)
+        if self.report is not None:
+            tmp = self.report + ".tmp"
+            with open(tmp, "w") as f:
+                f.write(str(self.calls))
+            os.replace(tmp, self.report)
+        return out
 
 
 def _dynamic_worker(rank, world, port, n, bs, out_dir, ck, slow, lanes):
@@ -493,7 +515,14 @@ def _dynamic_worker(rank, world, port, n, bs, out_dir, ck, slow, lanes):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     try:
         ref = pseudo_label(_StubModel(), _features, n, batch_size=bs, pad_token_id=PAD)  # per-round, static
-        m = _SlowModel(slow if rank == 0 else (), 0.4)
+        if "blocked" in slow:  # rank 0's first batch waits until rank 1 has decoded all the others
+            n_batches = len(shard_batches(n, bs, world, 0)) * world
+            peer, started = os.path.join(out_dir, "rank1_calls"), os.path.join(out_dir, "rank0_started")
+            # (rank 1's first batch waits until rank 0 holds one: otherwise a late rank 0 finds no batch left)
+            m = (_SlowModel(wait_for=(peer, n_batches - 1), announce=started) if rank == 0
+                 else _SlowModel(report=peer, wait_for=(started, 1)))
+        else:
+            m = _SlowModel(slow if rank == 0 else (), 0.4)
         if lanes > 1:
             m = _LaneStub()
         got = pseudo_label(m, _features, n, batch_size=bs, pad_token_id=PAD, gather="end", schedule="dynamic",
@@ -531,18 +560,19 @@ def test_dynamic_schedule_gloo_equals_static(tmp_path, n, bs, world, lanes):
 
 
 def test_dynamic_schedule_balances_a_slow_rank(tmp_path):
-    """Rank 0 draws a slow batch (0.4 s, as a three-pass batch costs twice a one-pass one): under the static plan it
-    would still decode half of the batches; with dynamic claims rank 1 takes the batches rank 0 is not ready for."""
+    """Rank 0's first batch is slow -- it does not return until rank 1 has decoded every other batch (a file rank 1's
+    model rewrites after each batch; ADVICE r05: an ordering, not a sleep, so a slow process start cannot change the
+    outcome): under the static plan rank 0 would still own half of the batches; with dynamic claims rank 1 decodes
+    all the batches rank 0 is not ready for, and the outputs are the reference's."""
     import json
 
     import torch.multiprocessing as mp
 
     n, bs = 16, 2  # 8 batches
-    # (rank 0's FIRST batch is the slow one: which batch a rank claims first is a race under dynamic claims)
-    mp.spawn(_dynamic_worker, args=(2, _free_port(), n, bs, str(tmp_path), "", ("first",), 1), nprocs=2, join=True)
+    mp.spawn(_dynamic_worker, args=(2, _free_port(), n, bs, str(tmp_path), "", ("blocked",), 1), nprocs=2, join=True)
     runs = [json.load(open(tmp_path / f"y{r}.json")) for r in range(2)]
     assert all(z["same"] for z in runs)
-    assert len(runs[1]["decoded"]) >= 5, runs  # rank 0 spent 0.4 s on batch 0: rank 1 took (nearly) all the rest
+    assert len(runs[0]["decoded"]) == 1 and len(runs[1]["decoded"]) == 7, runs
 
 
 def test_dynamic_schedule_resume_gloo_world2(tmp_path):

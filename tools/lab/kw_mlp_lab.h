@@ -1,5 +1,5 @@
 /* Lab-only ABI (not in libkwhisper.so): the fused decode feed-forward block, built by
- *   make -C kotoba-whisper_amd/csrc EXTRA=-DKW_LAB_MLP BUILD=build_mlp OUT=... TORCH_OUT=...
+ *   bash tools/lab/mlp_lab_build.sh "-DKW_LAB_MLP"   (product sources + tools/lab/lab_switches.diff)
  * and driven by tools/lab/mlp_coresident.py.  It lost to the two kw_dec_linear launches in rounds 4 and 5
  * (profiles/r05b_mlp_decomposition.txt), so the product library does not carry it. */
 #pragma once

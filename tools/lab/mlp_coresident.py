@@ -2,11 +2,12 @@
 """Lab driver (not product): the fused decode feed-forward block kw_dec_mlp against the two kw_dec_linear launches.
 
 The fused block lost in rounds 4 and 5 (profiles/r05b_mlp_decomposition.txt), so libkwhisper.so no longer carries
-it; the kernel stays in kotoba-whisper_amd/csrc/declin.hip behind KW_LAB_MLP.  Build a lab library and point this at it:
+it; the kernel lives in tools/lab/lab_switches.diff (behind KW_LAB_MLP once applied).  Build a lab library and point
+this at it:
 
-    make -C kotoba-whisper_amd/csrc EXTRA=-DKW_LAB_MLP BUILD=build_mlp OUT=$PWD/build_mlp/libkwhisper.so \\
-         TORCH_OUT=$PWD/build_mlp/libkwhisper_torch.so
-    KWHISPER_LIB=$PWD/build_mlp/libkwhisper.so KWHISPER_TORCH_LIB=$PWD/build_mlp/libkwhisper_torch.so \\
+    bash tools/lab/mlp_lab_build.sh "-DKW_LAB_MLP"
+    KWHISPER_LIB=$PWD/kotoba-whisper_amd/kwhisper/libkwhisper_lab.so \\
+    KWHISPER_TORCH_LIB=$PWD/kotoba-whisper_amd/kwhisper/libkwhisper_torch_lab.so \\
          python tools/lab/mlp_coresident.py [--check] [--reps 40]
 
 --check: h within f32 summation order of the two launches (fc1 is dec_linear's arithmetic; fc2 sums K in its own
