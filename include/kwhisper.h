@@ -29,7 +29,7 @@ enum { KW_DT_F32 = 0, KW_DT_BF16 = 1 };
 enum { KW_EPI_STORE = 0, KW_EPI_RESID = 1, KW_EPI_HEADSPLIT = 2 };
 
 /* ABI version (major*100 + minor) and the last error message of this thread. */
-int kw_version(void);  /* 111 */
+int kw_version(void);  /* 112 */
 const char* kw_last_error(void);
 
 /* A new non-blocking stream of its own (hipStreamCreateWithFlags), for callers that must not share one: the streams a
@@ -293,6 +293,22 @@ typedef struct {
 
 int kw_greedy_step(const kw_sampler_args* args, kw_stream_t stream);
 size_t kw_greedy_step_workspace(int64_t B);
+
+/* The LM head and the greedy step of one decode step in ONE launch (no timestamps): kw_dec_linear(lm) -- the final
+ * LayerNorm folded, proj_out (TF modeling_whisper.py:790,1080) -- followed by kw_greedy_step (TF generation/
+ * utils.py:2894-2937: SuppressTokens, SuppressTokensAtBegin, argmax, finished rows emit pad, stopping) without the
+ * kernel boundary: every workgroup of the LM head's weight stream publishes, per row, the processed arg-max of its
+ * run of columns, and the last one to arrive merges them and finishes the step.  The token is kw_greedy_step's
+ * (first index among equal maxima; a NaN logit never wins).
+ *   lm: a kw_dec_linear LM head -- LayerNorm-fused (ln = 1) STORE, M = B <= 32 rows; lm->C: f32 logits [B][ldc], or
+ *       NULL to skip storing them (the greedy step needs only the arg-max);
+ *   g:  a kw_sampler_args of the same B x V with return_timestamps = 0 and scores_out = NULL; g->logits and
+ *       g->counter are not used; g->workspace >= kw_dec_lm_greedy_workspace(B, V) bytes, ZERO-FILLED before first
+ *       use (every launch re-arms it).
+ * kw_dec_lm_greedy_supported(B, V, d): 1 when the shape is covered (else use kw_dec_linear + kw_greedy_step). */
+int kw_dec_lm_greedy(const kw_dec_linear_args* lm, const kw_sampler_args* g, kw_stream_t stream);
+size_t kw_dec_lm_greedy_workspace(int64_t B, int64_t V);
+int kw_dec_lm_greedy_supported(int64_t B, int64_t V, int64_t d);
 
 /* ---- beam search step (a10: TF/generation/utils.py:3208-3527), num_return_sequences = 1 ----------
  * Running rows are R = B * num_beams, item-major (row = b * num_beams + beam).  One step is

@@ -16,7 +16,7 @@ int kw_set_error_msg(int code, const char* msg) {
   return code;
 }
 
-extern "C" int kw_version(void) { return 111; }
+extern "C" int kw_version(void) { return 112; }
 
 extern "C" int kw_stream_create(kw_stream_t* out) {
   if (!out) return kw_set_error_msg(KW_EINVAL, "kw_stream_create: null out");

@@ -765,11 +765,123 @@ __device__ __forceinline__ void lmh_barrier() {  // LDS writes visible, then s_b
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg) {
+// The greedy step fused into the LM head (AM = true, kw_dec_lm_greedy; TF generation/utils.py:2894-2937 without
+// timestamps): each workgroup, after its run's logits are staged in LDS, takes every row's processed arg-max over the
+// run's columns (SuppressTokens, SuppressTokensAtBegin when L == begin_index; first index on ties) and publishes it as
+// one 8-byte {value, index} partial (sc1 store); the last workgroup to arrive (one agent-scope counter, MI355X_MICROARCH
+// "Valid forms" row 1) merges each row's partials -- the comparison (value, then lower index) is a total order, so the
+// token is the one kw_greedy_step's slice-ordered merge picks, NaN never winning -- and finishes the step exactly as
+// greedy_step_split_kernel does (finished -> pad, ids[L], unfinished, n_unfinished, cur_len).  The logits store is
+// optional (C may be null).
+struct LmGreedy {
+  const uint8_t* mask;     // [V] SuppressTokens
+  const int32_t* bsup;     // SuppressTokensAtBegin ids
+  int nbsup;
+  int64_t* ids;
+  int64_t ids_stride;
+  int32_t* cur_len;
+  int max_length, begin_index, eos_id, pad_id;
+  int32_t* unfinished;
+  int32_t* n_unfinished;
+  unsigned long long* part;  // [M][gridDim.x] {f32 value bits, int32 index}
+  int* arrive;               // arrival counter (zero before first use; re-armed by the last arriver)
+  int* fin;                  // [M] row r's finished flag, published by workgroup r
+};
+
+// (value, index) order of the arg-max: greater value, then lower index; NaN never wins (kw_greedy_step's compares)
+__device__ __forceinline__ void am_take(float& best, int& bi, float s, int v) {
+  if (s > best || (s == best && v < bi)) {
+    best = s;
+    bi = v;
+  }
+}
+__device__ __forceinline__ unsigned long long am_pack(float best, int bi) {
+  return (unsigned long long)__float_as_uint(best) | ((unsigned long long)(unsigned)bi << 32);
+}
+
+// AM epilogue: the run's partial arg-max per row, the arrival count, and in the last workgroup the merge and the step
+// bookkeeping.  Row r of a 16-lane group: lanes j = 0..15 take the run's columns j, j + 16, ...
+template <int OBW>
+__device__ __forceinline__ void lm_greedy_tail(const LmGreedy& sg, const float (*obuf)[OBW], const uint8_t* smask,
+                                               int ncol, int n0, int M, int L, int row_fin) {
+  const int tid = threadIdx.x, j = tid & 15, nth = blockDim.x;
+  const bool first = L == sg.begin_index;
+  const int G = gridDim.x;
+  for (int r = tid >> 4; r < M; r += nth >> 4) {
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int col = j; col < ncol; col += 16) {
+      const int n = n0 + col;
+      float s = smask[col] ? -INFINITY : obuf[r][col];
+      if (first)
+        for (int i = 0; i < sg.nbsup; ++i)
+          if (sg.bsup[i] == n) s = -INFINITY;
+      am_take(best, bi, s, n);
+    }
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      am_take(best, bi, ob, oi);
+    }
+    if (j == 0)
+      __hip_atomic_store(sg.part + (int64_t)r * G + blockIdx.x, am_pack(best, bi), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0 && (int)blockIdx.x < M) __hip_atomic_store(sg.fin + blockIdx.x, row_fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave's partials drained before the barrier
+  __shared__ int am_last, am_nunf;
+  __syncthreads();
+  if (tid == 0) {
+    am_nunf = 0;
+    am_last = __hip_atomic_fetch_add(sg.arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1;
+  }
+  __syncthreads();
+  if (!am_last) return;
+  // the last arriver: row r's G partials over its 16 lanes and its finished flag (sc1 loads, all in flight before
+  // the compares), then the step's bookkeeping
+  int n_unf = 0;
+  for (int r = tid >> 4; r < M; r += nth >> 4) {
+    constexpr int PQ = 16;  // partials per lane: G <= 256 (host-checked)
+    unsigned long long pv[PQ];
+#pragma unroll
+    for (int q = 0; q < PQ; ++q)
+      pv[q] = __hip_atomic_load(sg.part + (int64_t)r * G + min(j + 16 * q, G - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int fin = __hip_atomic_load(sg.fin + r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+#pragma unroll
+    for (int q = 0; q < PQ; ++q)
+      if (j + 16 * q < G) am_take(best, bi, __uint_as_float((unsigned)pv[q]), (int)(pv[q] >> 32));
+#pragma unroll
+    for (int o = 8; o > 0; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      am_take(best, bi, ob, oi);
+    }
+    if (j == 0) {
+      if (bi == 0x7fffffff) bi = 0;  // all NaN (cannot happen with a sane model): torch.argmax -> 0
+      const int64_t tok = fin ? (int64_t)sg.pad_id : (int64_t)bi;
+      sg.ids[(int64_t)r * sg.ids_stride + L] = tok;
+      const int done = fin || tok == sg.eos_id || (L + 1) >= sg.max_length;
+      sg.unfinished[r] = done ? 0 : 1;
+      n_unf += done ? 0 : 1;
+    }
+  }
+  if (n_unf) atomicAdd(&am_nunf, n_unf);
+  __syncthreads();
+  if (tid == 0) {
+    *sg.n_unfinished = am_nunf;
+    __hip_atomic_store(sg.arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *sg.cur_len = L + 1;
+  }
+}
+
+template <bool AM>
+__global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg, LmGreedy sg) {
   DecP p = p0;  // blockIdx.z = 32-row chunk (beam rows), as in dec_linear_kernel
   p.M = min(32, p0.M - 32 * (int)blockIdx.z);
   p.x += (int64_t)32 * blockIdx.z * p0.ldx;
-  p.C = reinterpret_cast<float*>(p0.C) + (int64_t)32 * blockIdx.z * p0.ldc;
+  if (p0.C) p.C = reinterpret_cast<float*>(p0.C) + (int64_t)32 * blockIdx.z * p0.ldc;
   __shared__ f32x4 red[3][MAXW][LMH_NCB][2][64];  // per-wave partial tiles, one slot per group in flight
   __shared__ float rpart[MAXW][32][2];
   __shared__ float rstat[32][2];
@@ -805,12 +917,28 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   // then the first two groups' weights, so the LayerNorm phase waits on the activations alone
   const int ncon = (g1 - g0) * LMH_NCB * 16;  // this run's columns: thread t stages columns t + j * blockDim
   float con_cs[LMH_ECJ], con_bn[LMH_ECJ];
+  [[maybe_unused]] uint8_t con_mk[LMH_ECJ];
+  [[maybe_unused]] int step_len = 0;
+  __shared__ uint8_t smask[AM ? LMH_MAXG * LMH_NCB * 16 : 1];
 #pragma unroll
   for (int j = 0; j < LMH_ECJ; ++j) {  // (clamped, not skipped: no load under a branch, host-checked coverage)
     const int t = min(tid + j * (int)blockDim.x, ncon - 1);
     const int n = min(g0 * LMH_NCB * 16 + t, p.N - 1);
     con_cs[j] = p.ln_colsum[n];
     con_bn[j] = p.bias ? p.bias[n] : 0.f;
+    if constexpr (AM) con_mk[j] = sg.mask[n];
+  }
+  // AM: workgroup r < M scans row r's id history for EOS (stopping_criteria.py:75-77) while the weights stream --
+  // wave 0, positions begin + lane + 64 u, loads clamped into the row (no wait on cur_len before issuing them)
+  [[maybe_unused]] int row_fin = 0;
+  [[maybe_unused]] int64_t hist[AM ? 7 : 1];
+  if constexpr (AM) {
+    step_len = *sg.cur_len;
+    if ((int)blockIdx.x < M && wave == 0) {
+      const int64_t* ids = sg.ids + (int64_t)blockIdx.x * sg.ids_stride;
+#pragma unroll
+      for (int u = 0; u < 7; ++u) hist[u] = ids[min(sg.begin_index + lane + 64 * u, (int)sg.ids_stride - 1)];
+    }
   }
   // activation fragments of this wave's k-range, once (rows lane&15 and 16 + lane&15)
   bf16x8 a0[LMH_KTM], a1[LMH_KTM];
@@ -833,6 +961,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
       const int gi = t / (LMH_NCB * 16), c = (t / 16) % LMH_NCB, col = t % 16;
       econ[gi][c][0][col] = con_cs[j];
       econ[gi][c][1][col] = con_bn[j];
+      if constexpr (AM) smask[t] = con_mk[j];
     }
   }
   // a wave with fewer than LMH_KTM k-tiles multiplies zero activations for the rest (exact: 0 x w adds +0), so the
@@ -934,10 +1063,21 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   // floats = 256 B), non-temporal
   lmh_barrier();
   const int ncol = min(g1 * LMH_NCB * 16, p.N) - g0 * LMH_NCB * 16;
-  float* cbase = reinterpret_cast<float*>(p.C) + g0 * LMH_NCB * 16;
-  for (int i = tid; i < M * ncol; i += blockDim.x) {
-    const int m = i / ncol, col = i - m * ncol;
-    __builtin_nontemporal_store(obuf[m][col], cbase + (int64_t)m * p.ldc + col);
+  if (p.C) {
+    float* cbase = reinterpret_cast<float*>(p.C) + g0 * LMH_NCB * 16;
+    for (int i = tid; i < M * ncol; i += blockDim.x) {
+      const int m = i / ncol, col = i - m * ncol;
+      __builtin_nontemporal_store(obuf[m][col], cbase + (int64_t)m * p.ldc + col);
+    }
+  }
+  if constexpr (AM) {
+    if ((int)blockIdx.x < M && wave == 0) {
+      int f = 0;
+#pragma unroll
+      for (int u = 0; u < 7; ++u) f |= (sg.begin_index + lane + 64 * u < step_len && hist[u] == sg.eos_id) ? 1 : 0;
+      row_fin = __builtin_amdgcn_ballot_w64(f != 0) != 0;
+    }
+    lm_greedy_tail(sg, obuf, smask, ncol, g0 * LMH_NCB * 16, M, step_len, row_fin);
   }
 }
 
@@ -1081,7 +1221,84 @@ int lmh_groups_per_wg(int64_t N) {
   return (groups + ncu - 1) / ncu;
 }
 
+// the persistent LM head (lm_head_kernel) covers the shape: <= 8 waves of LMH_KTM k-tiles, <= LMH_MAXG groups per
+// workgroup, the run's epilogue constants staged by one pass of LMH_ECJ per thread
+bool lmh_fits(int64_t M, int64_t N, int nkt) {
+  const int per = lmh_groups_per_wg(N);
+  return (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && M <= LMH_MAX_ROWS && per <= LMH_MAXG &&
+         64 * ((nkt + LMH_KTM - 1) / LMH_KTM) * LMH_ECJ >= per * LMH_NCB * 16;
+}
+
+// kw_dec_lm_greedy's grid (one run of column groups per workgroup, as kw_dec_linear's LM head)
+int lmg_grid(int64_t N) {
+  const int groups = (int)((N + 16 * LMH_NCB - 1) / (16 * LMH_NCB)), per = lmh_groups_per_wg(N);
+  return (groups + per - 1) / per;
+}
+constexpr int LMG_MAXG = 256;  // workgroups whose partials the last arriver merges (16 per lane)
+
 }  // namespace
+
+extern "C" size_t kw_dec_lm_greedy_workspace(int64_t B, int64_t V) {
+  const int64_t groups = (V + 16 * LMH_NCB - 1) / (16 * LMH_NCB);  // >= the grid on any device
+  return 256 + (size_t)B * (size_t)std::min<int64_t>(groups, LMG_MAXG) * sizeof(unsigned long long);
+}
+
+extern "C" int kw_dec_lm_greedy_supported(int64_t B, int64_t V, int64_t d) {
+  return B >= 1 && B <= LMH_MAX_ROWS && V >= 8192 && d > 0 && d % 32 == 0 && lmh_fits(B, V, (int)(d / 32)) &&
+                 lmg_grid(V) <= LMG_MAXG
+             ? 1
+             : 0;
+}
+
+extern "C" int kw_dec_lm_greedy(const kw_dec_linear_args* a, const kw_sampler_args* g, kw_stream_t stream) {
+  if (!a || !g || !a->x || !a->W || !a->ln || !a->ln_colsum || a->K <= 0 || a->K % 32 != 0 || a->ldx % 8 != 0 ||
+      a->ldx < a->K || (uintptr_t)a->x % 16 != 0 || a->epilogue != KW_EPI_STORE || a->gelu || a->scale_cols != 0 ||
+      (a->C && (a->c_dtype != KW_DT_F32 || a->ldc < a->N)))
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_lm_greedy: the LM head must be LayerNorm-fused STORE into f32 (or no) logits");
+  if (!g->suppress_mask || !g->ids || !g->cur_len || !g->unfinished || !g->n_unfinished || !g->workspace ||
+      (g->n_begin_suppress > 0 && !g->begin_suppress) || g->B != a->M || g->V != a->N)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_lm_greedy: sampler arguments missing or not the LM head's B x V");
+  if (g->return_timestamps || g->scores_out)
+    return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_lm_greedy: no timestamps, no scores_out (use kw_greedy_step)");
+  if (!kw_dec_lm_greedy_supported(a->M, a->N, a->K))
+    return kw_set_error_msg(KW_EUNSUPPORTED, "kw_dec_lm_greedy: shape not covered (kw_dec_lm_greedy_supported)");
+  if (g->ws_bytes < kw_dec_lm_greedy_workspace(a->M, a->N) || (uintptr_t)g->workspace % 16 != 0)
+    return kw_set_error_msg(KW_EINVAL, "kw_dec_lm_greedy: needs a zero-filled workspace of kw_dec_lm_greedy_workspace()");
+  DecP p{};
+  p.x = reinterpret_cast<const bf16_t*>(a->x);
+  p.ldx = a->ldx;
+  p.ln = 1;
+  p.ln_eps = a->ln_eps;
+  p.ln_colsum = a->ln_colsum;
+  p.W = reinterpret_cast<const bf16x8*>(a->W);
+  p.bias = a->bias;
+  p.C = a->C;
+  p.ldc = a->ldc;
+  p.M = (int)a->M;
+  p.N = (int)a->N;
+  p.K = (int)a->K;
+  LmGreedy sg{};
+  sg.mask = g->suppress_mask;
+  sg.bsup = g->begin_suppress;
+  sg.nbsup = g->n_begin_suppress;
+  sg.ids = g->ids;
+  sg.ids_stride = g->ids_stride;
+  sg.cur_len = g->cur_len;
+  sg.max_length = g->max_length;
+  sg.begin_index = g->begin_index;
+  sg.eos_id = g->eos_id;
+  sg.pad_id = g->pad_id;
+  sg.unfinished = g->unfinished;
+  sg.n_unfinished = g->n_unfinished;
+  sg.arrive = reinterpret_cast<int*>(g->workspace);
+  sg.fin = reinterpret_cast<int*>(g->workspace) + 32;
+  sg.part = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(g->workspace) + 256);
+  const int nkt = (int)(a->K / 32), nwv = (nkt + LMH_KTM - 1) / LMH_KTM;
+  hipLaunchKernelGGL(lm_head_kernel<true>, dim3((unsigned)lmg_grid(a->N)), dim3((unsigned)(64 * nwv)), 0,
+                     (hipStream_t)stream, p, lmh_groups_per_wg(a->N), sg);
+  KW_CHECK_LAUNCH();
+  return KW_OK;
+}
 
 extern "C" size_t kw_dec_linear_workspace_bytes(int64_t N, int64_t K) {
   const Geo g = choose(N, K);
@@ -1146,9 +1363,7 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? KW_OK : kw_set_error(e);
   }
-  const bool lmh = lm_shape && (nkt + LMH_KTM - 1) / LMH_KTM <= MAXW && a->M <= LMH_MAX_ROWS &&
-                   lmh_groups_per_wg(a->N) <= LMH_MAXG &&
-                   64 * ((nkt + LMH_KTM - 1) / LMH_KTM) * LMH_ECJ >= lmh_groups_per_wg(a->N) * LMH_NCB * 16;
+  const bool lmh = lm_shape && lmh_fits(a->M, a->N, nkt);
   // rows: one launch with a grid z-slice per 32-row chunk (K-split launches: up to ZMAX chunks each)
   const int64_t step = (g.ks == 1 || lmh) ? a->M : 32 * ZMAX;
   for (int64_t m0 = 0; m0 < a->M; m0 += step) {
@@ -1179,8 +1394,8 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
       const int groups = (int)((a->N + 16 * LMH_NCB - 1) / (16 * LMH_NCB));
       const int per = lmh_groups_per_wg(a->N);
       const int nwv = (nkt + LMH_KTM - 1) / LMH_KTM;
-      hipLaunchKernelGGL(lm_head_kernel, dim3((unsigned)((groups + per - 1) / per), 1, (unsigned)((p.M + 31) / 32)),
-                         dim3((unsigned)(64 * nwv)), 0, s, p, per);
+      hipLaunchKernelGGL(lm_head_kernel<false>, dim3((unsigned)((groups + per - 1) / per), 1, (unsigned)((p.M + 31) / 32)),
+                         dim3((unsigned)(64 * nwv)), 0, s, p, per, LmGreedy{});
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return kw_set_error(e);
       continue;

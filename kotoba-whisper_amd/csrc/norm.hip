@@ -1,4 +1,5 @@
 // LayerNorm, conv-stem re-layout and decoder embedding (HBM-bound row kernels).
+#include <algorithm>
 #include "kw_common.h"
 
 namespace {
@@ -188,6 +189,34 @@ __global__ __launch_bounds__(256) void mel_tm_kernel(const float* __restrict__ m
 }
 
 // ---- decoder embedding: h = tok_emb[id] + pos_emb[pos] (f32 residual stream) ----------------------
+// bf16 tables, d % 8 == 0, 16-B aligned rows: each thread one 8-column piece (16-B loads of both tables, two 16-B f32
+// stores and one 16-B bf16 store); the same per-element arithmetic as embed_kernel below (bitwise equal)
+__global__ __launch_bounds__(256) void embed_bf16x8_kernel(const int64_t* __restrict__ ids, int64_t ids_stride, int q_len,
+                                                           const int32_t* __restrict__ cur_len, const bf16_t* __restrict__ tok,
+                                                           const bf16_t* __restrict__ pos, int d, float* __restrict__ h,
+                                                           bf16_t* __restrict__ hb) {
+  const int r = blockIdx.x;  // b*q_len + i
+  const int b = r / q_len, i = r - b * q_len;
+  const int p = *cur_len - q_len + i;
+  const int64_t id = ids[(int64_t)b * ids_stride + p];
+  for (int c = 8 * threadIdx.x; c < d; c += 8 * blockDim.x) {
+    const u32x4 t4 = *reinterpret_cast<const u32x4*>(tok + id * d + c);
+    const u32x4 p4 = *reinterpret_cast<const u32x4*>(pos + (int64_t)p * d + c);
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      v[2 * e] = __uint_as_float(t4[e] << 16) + __uint_as_float(p4[e] << 16);
+      v[2 * e + 1] = __uint_as_float(t4[e] & 0xffff0000u) + __uint_as_float(p4[e] & 0xffff0000u);
+    }
+    float* hr = h + (int64_t)r * d + c;
+    *reinterpret_cast<f32x4*>(hr) = f32x4{v[0], v[1], v[2], v[3]};
+    *reinterpret_cast<f32x4*>(hr + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    if (hb)
+      *reinterpret_cast<u32x4*>(hb + (int64_t)r * d + c) =
+          u32x4{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7])};
+  }
+}
+
 template <typename TW>
 __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, int64_t ids_stride, int q_len,
                                                     const int32_t* __restrict__ cur_len, const TW* __restrict__ tok,
@@ -262,7 +291,14 @@ extern "C" int kw_embed(int dtype, const int64_t* ids, int64_t ids_stride, int64
     return kw_set_error_msg(KW_EINVAL, "kw_embed: invalid arguments");
   hipStream_t s = (hipStream_t)stream;
   dim3 grid((unsigned)(B * q_len));
-  if (dtype == KW_DT_F32)
+  const bool vec = dtype == KW_DT_BF16 && d % 8 == 0 && (uintptr_t)tok_emb % 16 == 0 && (uintptr_t)pos_emb % 16 == 0 &&
+                   (uintptr_t)h % 16 == 0 && (uintptr_t)hb % 16 == 0;
+  if (vec) {
+    const int64_t pieces = d / 8;
+    const unsigned threads = (unsigned)std::min<int64_t>(256, (pieces + 63) / 64 * 64);
+    hipLaunchKernelGGL(embed_bf16x8_kernel, grid, dim3(threads), 0, s, ids, ids_stride, (int)q_len, cur_len,
+                       (const bf16_t*)tok_emb, (const bf16_t*)pos_emb, (int)d, h, (bf16_t*)hb);
+  } else if (dtype == KW_DT_F32)
     hipLaunchKernelGGL(embed_kernel<float>, grid, dim3(256), 0, s, ids, ids_stride, (int)q_len, cur_len,
                        (const float*)tok_emb, (const float*)pos_emb, (int)d, h, (bf16_t*)hb);
   else

@@ -321,6 +321,50 @@ void greedy_step(Tensor& logits, const Tensor& suppress_mask, const optional<Ten
   check(kw_greedy_step(&a, stream_of(logits)), w);
 }
 
+// ---- LM head + greedy step in one launch (no timestamps) ------------------------------------------------
+// lm_geo = [x_offset, ldx, M, N, K]; cfg = [eos_id, pad_id, max_length, begin_index]
+void dec_lm_greedy(const Tensor& x, const Tensor& W, const optional<Tensor>& bias, const Tensor& ln_colsum,
+                   optional<Tensor> logits, const Tensor& suppress_mask, const optional<Tensor>& begin_suppress,
+                   Tensor& ids, Tensor& cur_len, Tensor& unfinished, Tensor& n_unfinished, Tensor& workspace,
+                   std::vector<int64_t> lm_geo, double ln_eps, std::vector<int64_t> cfg) {
+  const char* w = "kw_dec_lm_greedy";
+  dev(x, w), dev(W, w), dev(bias, w), dev(ln_colsum, w), dev(logits, w), dev(suppress_mask, w), dev(begin_suppress, w);
+  dev(ids, w), dev(cur_len, w), dev(unfinished, w), dev(n_unfinished, w), dev(workspace, w);
+  TORCH_CHECK_VALUE(lm_geo.size() == 5 && cfg.size() == 4, "kw_dec_lm_greedy: lm_geo holds 5, cfg 4 integers");
+  TORCH_CHECK_VALUE(x.scalar_type() == at::kBFloat16 && W.scalar_type() == at::kBFloat16,
+                    "kw_dec_lm_greedy takes bf16 activations and packed bf16 weights");
+  kw_dec_linear_args a{};
+  a.x = ptr(x, lm_geo[0]);
+  a.ldx = lm_geo[1];
+  a.ln = 1;
+  a.ln_eps = (float)ln_eps;
+  a.ln_colsum = ptr<const float>(ln_colsum);
+  a.W = ptr(W);
+  a.bias = optr<const float>(bias);
+  a.epilogue = KW_EPI_STORE;
+  a.C = optr<void>(logits);
+  a.ldc = logits.has_value() ? logits->stride(0) : lm_geo[3];
+  a.c_dtype = KW_DT_F32;
+  a.scale = 1.f;
+  a.M = lm_geo[2], a.N = lm_geo[3], a.K = lm_geo[4];
+  kw_sampler_args g{};
+  g.B = a.M, g.V = a.N;
+  g.suppress_mask = ptr<const uint8_t>(suppress_mask);
+  g.begin_suppress = optr<const int32_t>(begin_suppress);
+  g.n_begin_suppress = begin_suppress.has_value() ? (int32_t)begin_suppress->numel() : 0;
+  g.eos_id = (int32_t)cfg[0], g.pad_id = (int32_t)cfg[1], g.max_length = (int32_t)cfg[2], g.begin_index = (int32_t)cfg[3];
+  g.max_initial_ts = -1;
+  g.ids = ptr<int64_t>(ids);
+  g.ids_stride = ids.stride(0);
+  g.cur_len = ptr<int32_t>(cur_len);
+  g.unfinished = ptr<int32_t>(unfinished);
+  g.n_unfinished = ptr<int32_t>(n_unfinished);
+  g.workspace = ptr(workspace);
+  g.ws_bytes = (size_t)workspace.numel() * workspace.element_size();
+  c10::DeviceGuard dg(x.device());
+  check(kw_dec_lm_greedy(&a, &g, stream_of(x)), w);
+}
+
 // ---- beam search step ---------------------------------------------------------------------------------
 // cfg = [return_timestamps, ts_begin, no_ts_id, eos_id, max_initial_ts, begin_index, k]
 void beam_logprobs(const Tensor& logits, const Tensor& suppress_mask, const optional<Tensor>& begin_suppress,
@@ -399,6 +443,7 @@ int64_t workspace_bytes(std::string kind, std::vector<int64_t> d) {
   if (kind == "self_attn") return (int64_t)kw_self_attn_workspace(n(0), n(1), n(2));
   if (kind == "cross_attn") return (int64_t)kw_cross_attn_workspace(n(0), n(1), n(2), n(3), n(4));
   if (kind == "greedy_step") return (int64_t)kw_greedy_step_workspace(n(0));
+  if (kind == "lm_greedy") return (int64_t)kw_dec_lm_greedy_workspace(n(0), n(1));
   if (kind == "qkv_self") return (int64_t)kw_dec_qkv_self_workspace(n(0), n(1));
   if (kind == "xq_cross") return (int64_t)kw_dec_xq_cross_workspace(n(0), n(1), n(2), n(3));
   if (kind == "beam_logprobs") return (int64_t)kw_beam_logprobs_workspace(n(0));
@@ -437,6 +482,9 @@ TORCH_LIBRARY(kw, m) {
   m.def("greedy_step(Tensor(a!) logits, Tensor suppress_mask, Tensor? begin_suppress, Tensor(b!) ids, "
         "Tensor(c!) cur_len, Tensor(d!) unfinished, Tensor(e!) counter, Tensor(f!) n_unfinished, "
         "Tensor(g!)? scores_out, Tensor(h!)? workspace, int[] cfg) -> ()");
+  m.def("dec_lm_greedy(Tensor x, Tensor W, Tensor? bias, Tensor ln_colsum, Tensor(a!)? logits, Tensor suppress_mask, "
+        "Tensor? begin_suppress, Tensor(b!) ids, Tensor(c!) cur_len, Tensor(d!) unfinished, Tensor(e!) n_unfinished, "
+        "Tensor(f!) workspace, int[] lm_geo, float ln_eps, int[] cfg) -> ()");
   m.def("beam_logprobs(Tensor logits, Tensor suppress_mask, Tensor? begin_suppress, Tensor ids, Tensor cur_len, "
         "Tensor(a!) cand_val, Tensor(b!) cand_idx, Tensor done, Tensor(c!)? workspace, int[] cfg) -> ()");
   m.def("beam_select(Tensor cand_val, Tensor cand_idx, Tensor(a!) ids, Tensor(b!)? bp, Tensor(c!) run_scores, "
@@ -459,6 +507,7 @@ TORCH_LIBRARY_IMPL(kw, CUDA, m) {
   m.impl("dec_qkv_self", &dec_qkv_self);
   m.impl("dec_xq_cross", &dec_xq_cross);
   m.impl("greedy_step", &greedy_step);
+  m.impl("dec_lm_greedy", &dec_lm_greedy);
   m.impl("beam_logprobs", &beam_logprobs);
   m.impl("beam_select", &beam_select);
 }

@@ -20,7 +20,8 @@ LIB_PATH = os.environ.get("KWHISPER_LIB") or os.path.join(os.path.dirname(os.pat
 TORCH_LIB_PATH = os.environ.get("KWHISPER_TORCH_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                                       "libkwhisper_torch.so")
 TORCH_OPS = ("log_mel", "mel_to_time_major", "gemm", "dec_linear", "pack_weight", "layernorm", "attention", "embed",
-             "self_attn_step", "dec_qkv_self", "dec_xq_cross", "cross_attn_step", "greedy_step", "beam_logprobs", "beam_select")
+             "self_attn_step", "dec_qkv_self", "dec_xq_cross", "cross_attn_step", "greedy_step", "dec_lm_greedy",
+             "beam_logprobs", "beam_select")
 
 KW_OK, KW_EINVAL, KW_EHIP, KW_EUNSUPPORTED = 0, 1, 2, 3
 KW_DT_F32, KW_DT_BF16 = 0, 1
@@ -144,6 +145,9 @@ EXPORTS = {
     "kw_cross_attn_status_offset": (ctypes.c_size_t, [c_i64, c_i64, c_i64, c_i64, c_i64]),
     "kw_greedy_step": (ctypes.c_int, [ctypes.POINTER(SamplerArgs), c_vp]),
     "kw_greedy_step_workspace": (ctypes.c_size_t, [c_i64]),
+    "kw_dec_lm_greedy": (ctypes.c_int, [ctypes.POINTER(DecLinearArgs), ctypes.POINTER(SamplerArgs), c_vp]),
+    "kw_dec_lm_greedy_workspace": (ctypes.c_size_t, [c_i64, c_i64]),
+    "kw_dec_lm_greedy_supported": (ctypes.c_int, [c_i64, c_i64, c_i64]),
     "kw_beam_logprobs": (ctypes.c_int, [ctypes.POINTER(BeamLogprobsArgs), c_vp]),
     "kw_beam_logprobs_workspace": (ctypes.c_size_t, [c_i64]),
     "kw_beam_select": (ctypes.c_int, [ctypes.POINTER(BeamSelectArgs), c_vp]),

@@ -102,6 +102,8 @@ class DecodeSession:
         self.samp_ws = torch.zeros((ops.greedy_step_workspace_bytes(R) + 3) // 4, device=dev, dtype=torch.float32)
         self._greedy_cfg = {}
         self._pinned = None
+        self._lmg_ws = None  # kw_dec_lm_greedy's partials + arrival counter (zeroed once; launches re-arm it)
+        self.lm_greedy_last = False
         self.last_steps = 0
         if enc is not None:
             self.set_encoder_output(enc)
@@ -385,7 +387,7 @@ class DecodeSession:
         key = (max_length, P, bool(return_timestamps), tuple(gen.suppress_tokens or ()),
                tuple(gen.begin_suppress_tokens or ()), gen.timestamp_begin, gen.no_timestamps_token_id,
                gen.eos_token_id, gen.pad_token_id, gen.max_initial_timestamp_index, bool(record_scores),
-               self.eng.prefill_streams)
+               self.eng.prefill_streams, self.eng.fuse_lm_greedy)
         cfg = self._greedy_cfg.get(key)
         if cfg is None:
             sup = torch.zeros((self.eng.shape.vocab_size,), dtype=torch.uint8)
@@ -430,10 +432,29 @@ class DecodeSession:
         fused = max_length <= 256  # every step's position < 256 (kw_dec_qkv_self's key range)
         step_seq = self._step_plans(1, fused=fused)
         self.fused_last = bool(fused and self.qs_ok)
+        # the step's LM head + greedy step as one launch (kw_dec_lm_greedy; no timestamps, no recorded scores)
+        tail = sampler
+        s = self.eng.shape
+        if (self.eng.packed and self.nb == 1 and self.eng.fuse_lm_greedy and not return_timestamps and not record_scores
+                and ops.lm_greedy_supported(B, s.vocab_size, s.d_model)):
+            tail = cfg.get("lm_greedy")
+            if tail is None:
+                if self._lmg_ws is None:
+                    self._lmg_ws = torch.zeros((ops.lm_greedy_workspace_bytes(B, s.vocab_size) + 3) // 4, device=dev,
+                                               dtype=torch.float32)
+                sa = sampler.args
+                tail = cfg["lm_greedy"] = ops.LmGreedyPlan(
+                    self._buffers(1)["hb"], self.eng.lm_w, B, s.vocab_size, s.d_model, ln=(s.layer_norm_eps, self.eng.lm_cs),
+                    bias=self.eng.lm_b, suppress_mask=sampler._keep[1], begin_suppress=sampler._keep[2], ids=self.ids,
+                    cur_len=self.cur_len, unfinished=self.unfinished, n_unfinished=self.n_unfinished, eos_id=sa.eos_id,
+                    pad_id=sa.pad_id, max_length=sa.max_length, begin_index=sa.begin_index, workspace=self._lmg_ws)
+            assert getattr(step_seq[-1], "tag", None) == "lm_head"
+            step_seq = step_seq[:-1]
+        self.lm_greedy_last = tail is not sampler
 
         def one_step():
             self._run(step_seq)
-            sampler()
+            tail()
 
         def capture(n):
             def steps():

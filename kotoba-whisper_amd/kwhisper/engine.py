@@ -64,7 +64,7 @@ class WhisperEngine:
     def __init__(self, shape: WhisperShape, state_dict: dict, *, dtype=torch.bfloat16, device="cuda",
                  generation_config: GenerationConstants | None = None, fuse_qkv_self: bool = True,
                  fuse_xq_cross: bool = True, encoder_streams: int = 2, prefill_streams: int = 2,
-                 steps_per_replay: int = 2):
+                 steps_per_replay: int = 2, fuse_lm_greedy: bool = True):
         if dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("dtype must be torch.bfloat16 or torch.float32")
         L.load()
@@ -90,6 +90,9 @@ class WhisperEngine:
         # greedy decode steps per hipGraph replay (DecodeSession.generate: one launch, one unfinished-count copy and
         # event per replay; the host's stop check keeps the same lag in steps)
         self.steps_per_replay = max(1, int(steps_per_replay))
+        # greedy bf16 decode steps without timestamps run the LM head and the greedy step as one kw_dec_lm_greedy
+        # launch (the same tokens; False keeps kw_dec_linear + kw_greedy_step)
+        self.fuse_lm_greedy = bool(fuse_lm_greedy)
         self.device = torch.device(device)
         if self.device.type != "cuda":
             raise ValueError("WhisperEngine runs on a cuda (HIP) device only")

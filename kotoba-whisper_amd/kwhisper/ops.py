@@ -72,6 +72,7 @@ def _ws_bytes(kind: str, *dims) -> int:
     fn = {"dec_linear": "kw_dec_linear_workspace_bytes", "packed_weight": "kw_packed_weight_bytes",
           "self_attn": "kw_self_attn_workspace", "cross_attn": "kw_cross_attn_workspace",
           "greedy_step": "kw_greedy_step_workspace", "beam_logprobs": "kw_beam_logprobs_workspace",
+          "lm_greedy": "kw_dec_lm_greedy_workspace",
           "qkv_self": "kw_dec_qkv_self_workspace", "xq_cross": "kw_dec_xq_cross_workspace",
           "qkv_self_status": "kw_dec_qkv_self_status_offset", "xq_cross_status": "kw_dec_xq_cross_status_offset",
           "cross_attn_status": "kw_cross_attn_status_offset"}[kind]
@@ -498,6 +499,62 @@ class SamplerPlan:
             _kw().greedy_step(*self._targs)
         else:
             L.check(_lib().kw_greedy_step(self._ref, _s()), "kw_greedy_step")
+
+
+def lm_greedy_workspace_bytes(B: int, V: int) -> int:
+    return _ws_bytes("lm_greedy", B, V)
+
+
+def lm_greedy_supported(B: int, V: int, d: int) -> bool:
+    """Whether kw_dec_lm_greedy covers the shape (B <= 32 rows, the persistent LM head's geometry)."""
+    return bool(_lib().kw_dec_lm_greedy_supported(int(B), int(V), int(d)))
+
+
+class LmGreedyPlan:
+    """A pre-built ``kw_dec_lm_greedy`` call: the LM head (final LayerNorm folded, as the ``DecLinearPlan`` with
+    ``ln`` it replaces) and the greedy step without timestamps (as ``SamplerPlan``) in one launch.  ``x``: hb
+    [M][ldx] bf16 (x_offset elements in); ``logits``: optional f32 [M][V] (None: not stored); ``workspace``
+    zero-filled (lm_greedy_workspace_bytes); the device state (ids, cur_len, unfinished, n_unfinished) is the
+    sampler's."""
+
+    def __init__(self, x, W, M, N, K, *, ln, bias, suppress_mask, begin_suppress, ids, cur_len, unfinished,
+                 n_unfinished, eos_id, pad_id, max_length, begin_index, workspace, logits=None, ldx=None, x_offset=0,
+                 tag="lm_greedy"):
+        eps, colsum = ln
+        _cuda(x, W, bias, colsum, logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, n_unfinished,
+              workspace)
+        if x.dtype != torch.bfloat16 or W.dtype != torch.bfloat16:
+            raise ValueError("kw_dec_lm_greedy takes bf16 activations and packed bf16 weights")
+        if workspace.numel() * workspace.element_size() < lm_greedy_workspace_bytes(M, N):
+            raise ValueError("kw_dec_lm_greedy workspace too small")
+        ldx = K if ldx is None else ldx
+        self.tag = tag
+        a = L.DecLinearArgs()
+        a.x, a.ldx, a.ln, a.ln_eps, a.ln_colsum = x.data_ptr() + x_offset * 2, ldx, 1, float(eps), colsum.data_ptr()
+        a.W, a.bias = W.data_ptr(), bias.data_ptr() if bias is not None else None
+        a.epilogue, a.C, a.ldc, a.c_dtype = L.KW_EPI_STORE, _p(logits), logits.stride(0) if logits is not None else N, L.KW_DT_F32
+        a.scale, a.M, a.N, a.K = 1.0, M, N, K
+        g = L.SamplerArgs()
+        g.B, g.V = M, N
+        g.suppress_mask = suppress_mask.data_ptr()
+        g.begin_suppress = begin_suppress.data_ptr() if begin_suppress is not None else None
+        g.n_begin_suppress = begin_suppress.numel() if begin_suppress is not None else 0
+        g.eos_id, g.pad_id, g.max_length, g.begin_index, g.max_initial_ts = eos_id, pad_id, max_length, begin_index, -1
+        g.ids, g.ids_stride, g.cur_len = ids.data_ptr(), ids.stride(0), cur_len.data_ptr()
+        g.unfinished, g.n_unfinished = unfinished.data_ptr(), n_unfinished.data_ptr()
+        g.workspace, g.ws_bytes = workspace.data_ptr(), workspace.numel() * workspace.element_size()
+        self._a, self._g = a, g
+        self._ra, self._rg = ctypes.byref(a), ctypes.byref(g)
+        self._keep = (x, W, bias, colsum, logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, n_unfinished,
+                      workspace)
+        self._targs = (x, W, bias, colsum, logits, suppress_mask, begin_suppress, ids, cur_len, unfinished, n_unfinished,
+                       workspace, [x_offset, ldx, M, N, K], float(eps), [eos_id, pad_id, max_length, begin_index])
+
+    def __call__(self):
+        if _BACKEND == "torch":
+            _kw().dec_lm_greedy(*self._targs)
+        else:
+            L.check(_lib().kw_dec_lm_greedy(self._ra, self._rg, _s()), "kw_dec_lm_greedy")
 
 
 class BeamStepPlan:

@@ -44,7 +44,7 @@ def test_version(lib):
 
     with open(os.path.join(ROOT, "include", "kwhisper.h")) as f:
         want = int(re.search(r"int kw_version\(void\);\s*/\*\s*(\d+)\s*\*/", f.read()).group(1))
-    assert lib.kw_version() == want == 111
+    assert lib.kw_version() == want == 112
 
 
 def _c_layout(struct, fields):

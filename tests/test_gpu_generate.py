@@ -431,6 +431,29 @@ def test_steps_per_replay_tokens_identical(tiny16, ts, eos):
     assert torch.equal(out[1], out[2]) and torch.equal(out[1], out[3])
 
 
+@pytest.mark.parametrize("eos", [None, 7656])
+def test_lm_greedy_tokens_identical(tiny16, eos):
+    """The LM head and the greedy step fused into one launch (kw_dec_lm_greedy, WhisperEngine.fuse_lm_greedy, the
+    default without timestamps) give exactly the tokens of kw_dec_linear + kw_greedy_step -- also when rows finish
+    early on EOS (pad after it, the stop count) -- and the fused launch really ran (lm_greedy_last)."""
+    g = torch.Generator(device="cuda").manual_seed(9)
+    feats = torch.randn(6, TINY.num_mel_bins, TINY.n_frames, device="cuda", generator=g) * 0.5
+    gen = generation_constants(TINY)
+    if eos is not None:
+        gen.eos_token_id = eos
+    kw = dict(language="ja", task="transcribe", return_timestamps=False, max_length=40, generation_config=gen)
+    eng = tiny16.engine
+    out = {}
+    try:
+        for fuse in (False, True):
+            eng.fuse_lm_greedy = fuse
+            out[fuse] = tiny16.generate(feats, **kw).cpu()
+            assert tiny16._sessions[(6, 1)].lm_greedy_last == fuse
+    finally:
+        eng.fuse_lm_greedy = True
+    assert torch.equal(out[False], out[True])
+
+
 @pytest.mark.parametrize("k", [1, 2, 3])
 def test_stop_check_fires_after_last_eos(tiny16, k):
     """The host stop check reads the unfinished-row count a few replays behind, from a pinned slot that first gets

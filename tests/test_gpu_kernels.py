@@ -753,8 +753,11 @@ def test_dec_linear_resid(M, N, K):
     assert torch.equal(outs[0], outs[1])
 
 
-def test_embed_mirror():
-    B, q, d, V = 3, 2, 384, 1000
+@pytest.mark.parametrize("B,q,d", [(3, 2, 384), (32, 1, 1280), (2, 4, 1280), (3, 1, 12)])
+def test_embed_mirror(B, q, d):
+    """h = tok_emb[id] + pos_emb[pos] in f32 and its bf16 mirror, bit for bit (the 16-B vector kernel for
+    d % 8 == 0 -- r06 -- and the element kernel for d = 12)."""
+    V = 1000
     tok = torch.randn(V, d, device="cuda").bfloat16()
     pos = torch.randn(448, d, device="cuda").bfloat16()
     ids = torch.randint(0, V, (B, 449), device="cuda")
@@ -762,9 +765,79 @@ def test_embed_mirror():
     h = torch.empty(B * q, d, device="cuda")
     hb = torch.empty(B * q, d, device="cuda", dtype=torch.bfloat16)
     ops.embed(ids, B, q, cur, tok, pos, h, hb)
-    ref = (tok[ids[:, 5:7]].float() + pos[5:7].float()).reshape(B * q, d)
-    torch.testing.assert_close(h, ref)
+    ref = (tok[ids[:, 7 - q:7]].float() + pos[7 - q:7].float()).reshape(B * q, d)
+    assert torch.equal(h, ref)
     assert torch.equal(hb, ref.bfloat16())
+
+
+@pytest.mark.parametrize("B,V,K", [(32, 51866, 1280), (5, 51866, 1280), (1, 51865, 1280), (17, 51865, 384)])
+def test_lm_greedy_equals_lm_head_then_sampler(B, V, K):
+    """kw_dec_lm_greedy (the LM head and the greedy step in one launch, r06) == kw_dec_linear(LM head) followed by
+    kw_greedy_step, over five steps: the same tokens (ties between duplicated weight rows -> the first index; the
+    SuppressTokens mask; SuppressTokensAtBegin on the first step; a row finished by EOS emitting pad; max_length), the
+    same cur_len / unfinished / n_unfinished bookkeeping, the logits bit for bit when stored, and the arrival counter
+    back at zero after every launch."""
+    torch.manual_seed(B + V + K)
+    P = 3
+    eos, pad = 50257, 50256
+    W = (torch.randn(V, K, device="cuda") / K ** 0.5).bfloat16()
+    W[51000] = W[eos]  # tie pairs: a later duplicate never wins over the earlier row
+    W[2000:2010] = W[1000:1010]
+    Wp = ops.pack_weight(W)
+    cs = ops.ln_colsum(W)
+    bias = 0.1 * torch.randn(V, device="cuda")
+    bias[51000] = bias[eos]
+    bias[2000:2010] = bias[1000:1010]
+    sup = torch.zeros(V, dtype=torch.uint8, device="cuda")
+    sup[torch.randint(0, V, (400,), device="cuda")] = 1
+    sup[[eos, 51000, 1005, 2005]] = 0
+    bsup = torch.tensor([220, eos], dtype=torch.int32, device="cuda")
+    x_steps = [(torch.randn(B, K, device="cuda") * 2 + 0.3).bfloat16() for _ in range(5)]
+    for b in range(0, B, 3):  # some rows strongly prefer EOS (tied with row 51000: EOS wins, the row finishes)
+        x_steps[1][b] = (W[eos].float() * 8).bfloat16()
+    for b in range(1, B, 3):  # ... and some the tied pair 1005 / 2005 (1005 wins)
+        x_steps[2][b] = (W[1005].float() * 8).bfloat16()
+    outs = []
+    for fused in (False, True):
+        ids = torch.zeros((B, 64), dtype=torch.int64, device="cuda")
+        ids[:, :P] = torch.tensor([50258, 50266, 50360])
+        cur = torch.tensor([P], dtype=torch.int32, device="cuda")
+        unf = torch.ones(B, dtype=torch.int32, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        nun = torch.zeros(1, dtype=torch.int32, device="cuda")
+        x = torch.empty(B, K, device="cuda", dtype=torch.bfloat16)
+        logits = torch.full((B, V), float("nan"), device="cuda")
+        logs = []
+        if fused:
+            ws = torch.zeros(ops.lm_greedy_workspace_bytes(B, V) // 4 + 1, device="cuda")
+            plan = ops.LmGreedyPlan(x, Wp, B, V, K, ln=(1e-5, cs), bias=bias, suppress_mask=sup, begin_suppress=bsup,
+                                    ids=ids, cur_len=cur, unfinished=unf, n_unfinished=nun, eos_id=eos, pad_id=pad,
+                                    max_length=P + 4, begin_index=P, workspace=ws, logits=logits)
+            steps = [plan]
+        else:
+            sws = torch.zeros(ops.greedy_step_workspace_bytes(B) // 4 + 1, device="cuda")
+            steps = [ops.DecLinearPlan(x, Wp, B, V, K, ln=(1e-5, cs), bias=bias, C=logits),
+                     ops.SamplerPlan(logits, sup, bsup, ids, cur, unf, cnt, nun, return_timestamps=False, ts_begin=50365,
+                                     no_ts_id=50364, eos_id=eos, pad_id=pad, max_initial_ts=None, max_length=P + 4,
+                                     begin_index=P, workspace=sws)]
+        for xs in x_steps:
+            x.copy_(xs)
+            for f in steps:
+                f()
+            logs.append(logits.clone())
+            if fused:
+                torch.cuda.synchronize()
+                assert int(ws.view(torch.int32)[0].item()) == 0  # arrival counter re-armed
+        torch.cuda.synchronize()
+        outs.append((ids.cpu(), int(cur.item()), unf.cpu(), int(nun.item()), logs))
+    (a_ids, a_cur, a_unf, a_nun, a_logs), (b_ids, b_cur, b_unf, b_nun, b_logs) = outs
+    assert torch.equal(a_ids, b_ids), (a_ids[:, P:P + 5], b_ids[:, P:P + 5])
+    assert (a_cur, a_nun) == (b_cur, b_nun) and torch.equal(a_unf, b_unf)
+    assert (a_ids[:, P:P + 5] == eos).any() and (a_ids[:, P:P + 5] == pad).any()  # EOS finished some rows
+    if B > 1:
+        assert (a_ids[:, P + 2] == 1005).any() and not (a_ids[:, P:P + 5] == 2005).any()
+    for la, lb in zip(a_logs, b_logs):
+        assert torch.equal(la, lb)
 
 
 @pytest.mark.parametrize("rt", [False, True])

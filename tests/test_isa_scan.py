@@ -38,7 +38,8 @@ CASES = {
     "beam.hip": [(r"beam_logprobs_split_kernel", 33)],
     # the LM head's run: epilogue constants + 10 activation fragments + two groups' weights + every prefetch of the
     # group loop before any vmcnt(0) (r05: the loop's joins no longer drain the prefetch)
-    "declin.hip": [(r"lm_head_kernel", 50)],
+    # (r06: the same run with the greedy step's mask bytes and cur_len beside the constants -- kw_dec_lm_greedy)
+    "declin.hip": [(r"lm_head_kernelILb0E", 50), (r"lm_head_kernelILb1E", 50)],
 }
 
 
