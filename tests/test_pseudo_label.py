@@ -628,3 +628,38 @@ def test_dynamic_schedule_single_process(lanes):
     assert sorted(tuple(b) for h in m.lanes for b in h.batches) == sorted(tuple(b) for b in shard_batches(23, 4, 1, 0))
     with pytest.raises(ValueError, match="schedule"):
         pseudo_label(_StubModel(), _features, 3, batch_size=4, pad_token_id=PAD, schedule="dynamic")
+
+
+def _bench_configs():
+    import importlib.util
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_configs", os.path.join(root, "tools", "bench_configs.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def test_dp_projection_pass_units():
+    """VERDICT r5 item 5's seek-pass work units (tools/bench_configs.py pass_unit_makespan): with every batch one
+    pass they are the dynamic batch schedule; with multi-pass batches they never lose to it, and on round 4's measured
+    config-4 per-batch times (four three-pass batches, the LAST batch among them) W = 8 stays at the dynamic
+    schedule's 0.84 -- the last batch's three dependent passes are the job's critical path."""
+    bc = _bench_configs()
+    rng = np.random.default_rng(3)
+    one = 0.4 + 0.01 * rng.random(56)
+    p1 = bc.dp_projection(one, passes=[1] * 56)
+    for w in ("w2", "w4", "w8"):
+        assert p1[w]["dynamic_pass_units"] == p1[w]["dynamic"]
+    t = np.full(56, 0.429)
+    passes = [1] * 56
+    for j in (0, 16, 50, 55):
+        t[j], passes[j] = 0.825, 3
+    pj = bc.dp_projection(t, passes=passes)
+    for w in ("w2", "w4", "w8"):
+        assert pj[w]["dynamic_pass_units"] >= pj[w]["dynamic"] - 1e-4
+    assert pj["w8"]["dynamic_pass_units"] < 0.86
+    # the same batches with the three-pass ones first: the passes then overlap other ranks' work
+    order = [0, 16, 50, 55] + [j for j in range(56) if j not in (0, 16, 50, 55)]
+    pf = bc.dp_projection(t[order], passes=[passes[j] for j in order])
+    assert pf["w8"]["dynamic_pass_units"] > 0.93

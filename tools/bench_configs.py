@@ -109,10 +109,45 @@ def config4(a, world, rank, dev):
                        "gather": a.gather, "lanes": a.lanes, "schedule": a.schedule, "weights": a.weights,
                        "tokens_per_clip_mean": float(np.mean([len(p) for p in preds]))},
             "batch_seconds": [round(float(x), 5) for x in batch_s], "batch_seek_passes": [passes[si] for si in sorted(passes)],
-            "dp_projection": dp_projection(batch_s) if world == 1 and a.lanes == 1 else None}
+            "dp_projection": (dp_projection(batch_s, passes=[passes[si] for si in sorted(passes)])
+                              if world == 1 and a.lanes == 1 else None)}
 
 
-def dp_projection(batch_s, worlds=(2, 4, 8)):
+def pass_unit_makespan(batch_s, passes, W):
+    """List scheduling over seek-PASS work units: a batch's first pass is a unit claimed in plan
+    order; each later pass of a multi-pass batch becomes a unit of its own once the previous pass has finished (rows
+    are independent -- a row's pass-k decode depends on the row, its seek and k alone: TF generation_whisper.py:785-903,
+    the max_length growth :1932-1940 is a function of the pass index; the engine is batch-invariant), claimed ahead of
+    fresh batches by the first idle rank.  One-pass batches cost their time; a p-pass batch of time T costs t1 (the
+    one-pass median) for pass 1 and (T - t1) / (p - 1) per later pass.  Returns the makespan."""
+    import heapq
+
+    t = np.asarray(batch_s, dtype=np.float64)
+    p = np.asarray(passes, dtype=np.int64)
+    t1 = float(np.median(t[p == 1])) if (p == 1).any() else float(t.min())
+    free = [0.0] * W
+    pending = []  # (ready time, cost, batch, pass index)
+    nxt, end = 0, 0.0
+    while nxt < len(t) or pending:
+        tf = heapq.heappop(free)
+        ready = [u for u in pending if u[0] <= tf]
+        if ready or nxt >= len(t):
+            u = min(ready or pending)
+            pending.remove(u)
+            fin = max(tf, u[0]) + u[1]
+            if u[3] + 1 < p[u[2]]:
+                pending.append((fin, u[1], u[2], u[3] + 1))
+        else:
+            b, nxt = nxt, nxt + 1
+            fin = tf + (t1 if p[b] > 1 else t[b])
+            if p[b] > 1:
+                pending.append((fin, (t[b] - t1) / (p[b] - 1), b, 1))
+        heapq.heappush(free, fin)
+        end = max(end, fin)
+    return end
+
+
+def dp_projection(batch_s, worlds=(2, 4, 8), passes=None):
     """Projected data-parallel efficiency at W ranks from W = 1 per-batch times.
     Global batch i runs on rank i % W (accelerate's shard plan; the wrapped duplicates of the last round are real
     work).  Lock step (the reference's per-batch gather, gather="round"): every round waits for its slowest batch,
@@ -139,6 +174,8 @@ def dp_projection(batch_s, worlds=(2, 4, 8)):
         out[f"w{W}"] = {"lockstep": round(float(r.mean(1).sum() / r.max(1).sum()), 4),
                         "deferred": round(float(tt.sum() / W / r.sum(0).max()), 4),
                         "dynamic": round(listed(tt), 4), "dynamic_x10": round(listed(np.tile(t, 10)), 4)}
+        if passes is not None:  # seek passes as work units (pass_unit_makespan), no wrap-around duplicates
+            out[f"w{W}"]["dynamic_pass_units"] = round(float(t.sum() / W / pass_unit_makespan(t, passes, W)), 4)
     return out
 
 

@@ -34,6 +34,9 @@ def main():
                     help="numpy: kwhisper.synthetic.synthetic_state_dict, the weights every transformers fixture uses; "
                     "torch: synthetic_state_dict_torch (the device generator: a DIFFERENT random model, which "
                     "transformers on the CPU cannot reproduce -- round 4's scan used it)")
+    ap.add_argument("--seed", type=int, default=0, help="the numpy recipe's seed (the fixture model is seed 0)")
+    ap.add_argument("--stop-after", type=int, default=0, help="stop once this many multi-pass clips were found (0: scan all)")
+    ap.add_argument("--first-clip", type=int, default=0, help="scan clips [first-clip, first-clip + n-clips)")
     ap.add_argument("--features-out", default="",
                     help="npz of the HIP log-mel of every multi-pass clip (+ up to 8 one-pass clips) for "
                     "tools/make_fixtures.py --only c4_hipmel")
@@ -44,15 +47,16 @@ def main():
     from kwhisper.synthetic import reazon_audio, reazon_durations, synthetic_state_dict, synthetic_state_dict_torch
 
     dev = torch.device("cuda", 0)
-    sd = synthetic_state_dict(LARGE_V3, 0) if a.weights == "numpy" else synthetic_state_dict_torch(LARGE_V3, seed=0, device=dev)
+    sd = (synthetic_state_dict(LARGE_V3, a.seed) if a.weights == "numpy"
+          else synthetic_state_dict_torch(LARGE_V3, seed=a.seed, device=dev))
     model = KWhisperForConditionalGeneration.from_state_dict(LARGE_V3, sd, dtype=getattr(torch, a.dtype), device=dev,
                                                              generation_config=generation_constants(LARGE_V3))
     del sd
     fe = WhisperFeatureExtractor(feature_size=LARGE_V3.num_mel_bins, device=dev)
-    durs = reazon_durations()[: a.n_clips]
+    durs = reazon_durations()[: a.first_clip + a.n_clips]
     passes, ntok, keep = [], [], {}
     t0 = time.time()
-    for b0 in range(0, len(durs), a.batch):
+    for b0 in range(a.first_clip, len(durs), a.batch):
         idx = list(range(b0, min(b0 + a.batch, len(durs))))
         audio = np.zeros((len(idx), 480000), np.float32)
         for j, i in enumerate(idx):
@@ -69,13 +73,16 @@ def main():
         ntok += (toks != pad).sum(1).cpu().tolist()
         print(f"batch {b0 // a.batch}: passes {model.stats['row_passes'].tolist()} ({time.time() - t0:.1f}s)",
               flush=True)
+        if a.stop_after and sum(1 for x in passes if x >= 2) >= a.stop_after:
+            break
     passes = np.array(passes)
     if a.features_out and keep:
         ids = sorted(keep)
         np.savez_compressed(a.features_out, clip_ids=np.asarray(ids, np.int64), durations=durs[ids].astype(np.float64),
                             features=np.stack([keep[i] for i in ids]).astype(np.float32))
-    res = {"dtype": a.dtype, "weights": a.weights, "n_clips": len(durs), "max_length": 128, "passes": passes.tolist(), "tokens": ntok,
-           "multipass_clips": np.nonzero(passes >= 2)[0].tolist(),
+    res = {"dtype": a.dtype, "weights": a.weights, "seed": a.seed, "first_clip": a.first_clip, "n_clips": len(passes),
+           "max_length": 128, "passes": passes.tolist(), "tokens": ntok,
+           "multipass_clips": (a.first_clip + np.nonzero(passes >= 2)[0]).tolist(),
            "histogram": {int(k): int((passes == k).sum()) for k in np.unique(passes)}}
     os.makedirs(os.path.dirname(a.out) or ".", exist_ok=True)
     with open(a.out, "w") as f:
