@@ -69,6 +69,7 @@ struct DecP {
   int* cnt;
   int xlds;  // stage the activation rows through LDS (single-round grids and split-K slices)
   int zrows; // rows per grid z-chunk: 32, or 16 for narrow grids (row split, launch())
+  int vec_epi;  // outputs in whole 16-B pieces (N % 16 == 0, 16-B aligned rows): the epilogue stores 16-B pieces
 };
 
 // H2: the second 16-row half of the tile exists (false: a row-split chunk of <= 16 rows -- its a1 / c1 / LayerNorm
@@ -252,16 +253,18 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     }
   }
 
-  // 5. K-split seam: publish the partial tile write-through, count arrivals, the last one sums in order
+  // 5. K-split seam: publish the partial tile write-through, count arrivals, the last one sums in order.  r06: each
+  //    lane's two accumulator quads go out as two 16-B sc1 stores and come back as 16-B sc1 loads (the 4-B sc1 stores
+  //    were one fabric write each, ~6x the 16-B form's time per byte: MI355X_MICROARCH "stores of each flavour"); the
+  //    same values summed in the same order.  Slab: [column group][K split][NCB][row half][64 lanes][4] f32
   if (ksn > 1) {
-    float* mine = p.slab + ((int64_t)cg * ksn + ks) * (NCB * 512);
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(p.slab + (int64_t)cg * ksn * (NCB * 512), (short)0,
+                                                                         ksn * NCB * 512 * 4, 0x00020000);
 #pragma unroll
-    for (int c = 0; c < NCB; ++c)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        __hip_atomic_store(mine + c * 512 + r * 64 + lane, c0[c][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(mine + c * 512 + 256 + r * 64 + lane, c1[c][r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+    for (int c = 0; c < NCB; ++c) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, c0[c]), srs, ((ks * NCB + c) * 128 + lane) * 16, 0, 16);
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, c1[c]), srs, ((ks * NCB + c) * 128 + 64 + lane) * 16, 0, 16);
+    }  // (aux 16 = sc1)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     int last = 0;
     if (lane == 0) {
@@ -271,27 +274,25 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     }
     last = __shfl(last, 0, 64);
     if (!last) return;
-    // every slab load in flight before the first add (fixed summation order q = 0, 1, ...)
-    const float* all = p.slab + (int64_t)cg * ksn * (NCB * 512);
-    float pv[KSMAX][NCB][8];
+    // every slab load in flight before the first add (fixed summation order q = 0, 1, ...); splits q >= ksn lie past
+    // the buffer's range and load zeros, as the 4-B form's 0.f did
+    f32x4 pv[KSMAX][NCB][2];
 #pragma unroll
     for (int q = 0; q < KSMAX; ++q)
 #pragma unroll
-      for (int c = 0; c < NCB; ++c)
-#pragma unroll
-        for (int e = 0; e < 8; ++e)
-          pv[q][c][e] = q < ksn ? __hip_atomic_load(all + q * NCB * 512 + c * 512 + (e >> 2) * 256 + (e & 3) * 64 + lane,
-                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                : 0.f;
+      for (int c = 0; c < NCB; ++c) {
+        pv[q][c][0] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, ((q * NCB + c) * 128 + lane) * 16, 0, 16));
+        pv[q][c][1] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(srs, ((q * NCB + c) * 128 + 64 + lane) * 16, 0, 16));
+      }
 #pragma unroll
     for (int c = 0; c < NCB; ++c)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float v0 = pv[0][c][r], v1 = pv[0][c][4 + r];
+        float v0 = pv[0][c][0][r], v1 = pv[0][c][1][r];
 #pragma unroll
         for (int q = 1; q < KSMAX; ++q) {
-          v0 += pv[q][c][r];
-          v1 += pv[q][c][4 + r];
+          v0 += pv[q][c][0][r];
+          v1 += pv[q][c][1][r];
         }
         c0[c][r] = v0;
         c1[c][r] = v1;
@@ -299,12 +300,11 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
   }
 
   KW_DEC_STAMP(3);
-  // 6. epilogue: MFMA C layout -> element (row 4*(lane>>4)+r [+16], column lane&15)
+  // 6. epilogue: MFMA C layout -> element (row 4*(lane>>4)+r [+16], column lane&15); from here on wave 0 runs alone
+  float vals[NCB][2][4];
 #pragma unroll
   for (int c = 0; c < NCB; ++c) {
-    const int cb = cg * NCB + c;
-    const int n = cb * 16 + (lane & 15);
-    const bool nvalid = n < p.N;
+    const int n = (cg * NCB + c) * 16 + (lane & 15);
     const float bn = ebias[c];
     const float cs = ecsum[c];
 #pragma unroll
@@ -312,22 +312,78 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = 16 * hh + 4 * (lane >> 4) + r;
-        const bool valid = nvalid && m < M;
         float v = hh ? c1[c][r] : c0[c][r];
         if constexpr (LNA) v = rstat[m][1] * (v - rstat[m][0] * cs);  // LN(x) W'^T
         v += bn;
         if constexpr (EPI == KW_EPI_RESID) {
           v += hold[c][hh][r];
-          if (valid) {
-            p.h[(int64_t)m * p.ldh + n] = v;
-            p.hb[(int64_t)m * p.ldh + n] = f2bf(v);
-          }
         } else {
           if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
           if (n < p.scale_cols) v *= p.scale;
-          if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
+        }
+        vals[c][hh][r] = v;
+      }
+    }
+  }
+  constexpr int R = H2 ? 32 : 16;  // rows of the tile
+  if (p.vec_epi) {
+    // r06: the tile staged row-major in the (now free) reduction buffer, then stored as whole 16-B pieces -- f32 rows
+    // 4 columns, bf16 rows 8 -- instead of 2-4-B stores of 16 columns x 4 rows per instruction (the same values)
+    constexpr int SW = NCB * 16 + 4;  // staging row stride (floats): the 4 rows of one write 16 banks apart
+    float* stg = reinterpret_cast<float*>(&red[0][0][0][0]);
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+#pragma unroll
+      for (int hh = 0; hh < (H2 ? 2 : 1); ++hh)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) stg[(16 * hh + 4 * (lane >> 4) + r) * SW + c * 16 + (lane & 15)] = vals[c][hh][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int n0 = cg * NCB * 16;
+    constexpr bool F32 = EPI == KW_EPI_RESID || sizeof(TC) == 4, BF16 = EPI == KW_EPI_RESID || sizeof(TC) == 2;
+    if constexpr (F32) {
+      float* dst = EPI == KW_EPI_RESID ? p.h : reinterpret_cast<float*>(p.C);
+      const int64_t ld = EPI == KW_EPI_RESID ? p.ldh : p.ldc;
+#pragma unroll
+      for (int i = 0; i < (R * NCB * 4 + 63) / 64; ++i) {
+        const int pc = lane + 64 * i, m = pc / (NCB * 4), q = pc - m * (NCB * 4);
+        if (pc < R * NCB * 4 && m < M && n0 + 4 * q < p.N)
+          *reinterpret_cast<f32x4*>(dst + (int64_t)m * ld + n0 + 4 * q) = *reinterpret_cast<const f32x4*>(stg + m * SW + 4 * q);
+      }
+    }
+    if constexpr (BF16) {
+      bf16_t* dst = EPI == KW_EPI_RESID ? p.hb : reinterpret_cast<bf16_t*>(p.C);
+      const int64_t ld = EPI == KW_EPI_RESID ? p.ldh : p.ldc;
+#pragma unroll
+      for (int i = 0; i < (R * NCB * 2 + 63) / 64; ++i) {
+        const int pc = lane + 64 * i, m = pc / (NCB * 2), q = pc - m * (NCB * 2);
+        if (pc < R * NCB * 2 && m < M && n0 + 8 * q < p.N) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(stg + m * SW + 8 * q);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(stg + m * SW + 8 * q + 4);
+          *reinterpret_cast<u32x4*>(dst + (int64_t)m * ld + n0 + 8 * q) =
+              u32x4{pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(b[0], b[1]), pack_bf16x2(b[2], b[3])};
         }
       }
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      const int n = (cg * NCB + c) * 16 + (lane & 15);
+#pragma unroll
+      for (int hh = 0; hh < (H2 ? 2 : 1); ++hh)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = 16 * hh + 4 * (lane >> 4) + r;
+          if (n >= p.N || m >= M) continue;
+          const float v = vals[c][hh][r];
+          if constexpr (EPI == KW_EPI_RESID) {
+            p.h[(int64_t)m * p.ldh + n] = v;
+            p.hb[(int64_t)m * p.ldh + n] = f2bf(v);
+          } else {
+            TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v);
+          }
+        }
     }
   }
   KW_DEC_STAMP(4);
@@ -1390,6 +1446,11 @@ extern "C" int kw_dec_linear(const kw_dec_linear_args* a, kw_stream_t stream) {
     p.cnt = reinterpret_cast<int*>(a->workspace);
     p.slab = a->workspace ? reinterpret_cast<float*>(reinterpret_cast<char*>(a->workspace) + CNT_MAX * sizeof(int)) : nullptr;
     p.xlds = use_xlds(a->N, g) ? 1 : 0;
+    // 16-B epilogue pieces: whole 16-column blocks and 16-B aligned rows (every z-chunk's rows too)
+    p.vec_epi = a->N % 16 == 0 &&
+                (a->epilogue == KW_EPI_RESID
+                     ? a->ldh % 8 == 0 && (uintptr_t)p.h % 16 == 0 && (uintptr_t)p.hb % 16 == 0
+                     : (a->ldc * (int64_t)csz) % 16 == 0 && (uintptr_t)p.C % 16 == 0);
     if (lmh) {
       const int groups = (int)((a->N + 16 * LMH_NCB - 1) / (16 * LMH_NCB));
       const int per = lmh_groups_per_wg(a->N);
