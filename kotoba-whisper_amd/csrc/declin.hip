@@ -129,6 +129,10 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
   // epilogue operands of wave 0 (lane <-> column lane&15, rows 4*(lane>>4)+r and 16+...), loaded with
   // the operands so the epilogue never waits on a memory round trip: bias, LayerNorm column sums and
   // (RESID) the residual rows
+  // r06: with the epilogue spread over the tile's J = NCB x row-half jobs (one wave each: step 4), every job wave
+  // loads the residual rows too (16 floats per lane from L2; it keeps only its job's four)
+  constexpr int HH = H2 ? 2 : 1, J = NCB * HH;
+  const bool spread = J > 1 && ksn == 1 && nw >= J;
   float hold[NCB][2][4], ebias[NCB], ecsum[NCB];
 #pragma unroll
   for (int c = 0; c < NCB; ++c) {
@@ -137,7 +141,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
     ecsum[c] = LNA ? p.ln_colsum[n] : 0.f;
   }
   if constexpr (EPI == KW_EPI_RESID) {
-    if (wave == 0) {
+    if (spread ? wave < J : wave == 0) {
 #pragma unroll
       for (int c = 0; c < NCB; ++c) {
         const int n = min((cg * NCB + c) * 16 + (lane & 15), p.N - 1);
@@ -224,6 +228,111 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
 
   // 4. reduce the waves' K slices (fixed order); wave 0 continues
   KW_DEC_STAMP(2);
+  if (spread) {
+    // r06: the tile's J (column block, row half) jobs -- fc1: 4 -- on waves 0..J-1 at once, each summing its 16 x 16
+    // partial tiles in wave order, forming its row half's LayerNorm statistics itself and storing its piece (LDS is in
+    // order within a wave; two jobs of one half write the same values): bitwise wave 0 alone, as the rows kernel's
+    // spread epilogue (dec_linear_rows_kernel) -- fc1's reduction + epilogue 2.0 us on one wave (profiles/r06f_*)
+    __shared__ __attribute__((aligned(16))) float stg[J][16][20];
+#pragma unroll
+    for (int c = 0; c < NCB; ++c) {
+      red[wave][c][0][lane] = c0[c];
+      if constexpr (H2) red[wave][c][1][lane] = c1[c];
+    }
+    __syncthreads();
+    if (wave >= J) return;
+    const int cj = wave / HH, hj = wave - cj * HH;
+    if constexpr (LNA) {
+      if (lane < 16) {
+        const int m = 16 * hj + lane;
+        float sx = 0.f, sq = 0.f;
+        for (int w2 = 0; w2 < nw; ++w2) {
+          sx += rpart[w2][m][0];
+          sq += rpart[w2][m][1];
+        }
+        const float inv = 1.f / (float)p.K;
+        const float mean = sx * inv;
+        rstat[m][0] = mean;
+        rstat[m][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + p.ln_eps);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    f32x4 acc = red[0][cj][hj][lane];
+    for (int w2 = 1; w2 < nw; ++w2) acc += red[w2][cj][hj][lane];
+    KW_DEC_STAMP(3);
+    float bn = 0.f, cs = 0.f, hv[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCB; ++c)
+      if (c == cj) {
+        bn = ebias[c];
+        cs = ecsum[c];
+#pragma unroll
+        for (int hh = 0; hh < HH; ++hh)
+          if (hh == hj)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) hv[r] = hold[c][hh][r];
+      }
+    const int nb = (cg * NCB + cj) * 16;  // the job's first column
+    const int n = nb + (lane & 15);
+    float v4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = 16 * hj + 4 * (lane >> 4) + r;
+      float v = acc[r];
+      if constexpr (LNA) v = rstat[m][1] * (v - rstat[m][0] * cs);
+      v += bn;
+      if constexpr (EPI == KW_EPI_RESID) {
+        v += hv[r];
+      } else {
+        if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
+        if (n < p.scale_cols) v *= p.scale;
+      }
+      v4[r] = v;
+    }
+    if (p.vec_epi) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) stg[wave][4 * (lane >> 4) + r][lane & 15] = v4[r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      constexpr bool F32 = EPI == KW_EPI_RESID || sizeof(TC) == 4, BF16 = EPI == KW_EPI_RESID || sizeof(TC) == 2;
+      if constexpr (F32) {  // 16 rows x 4 pieces: one per lane
+        float* dst = EPI == KW_EPI_RESID ? p.h : reinterpret_cast<float*>(p.C);
+        const int64_t ld = EPI == KW_EPI_RESID ? p.ldh : p.ldc;
+        const int ml = lane >> 2, q = lane & 3, m = 16 * hj + ml;
+        if (m < M && nb + 4 * q < p.N)
+          *reinterpret_cast<f32x4*>(dst + (int64_t)m * ld + nb + 4 * q) = *reinterpret_cast<const f32x4*>(&stg[wave][ml][4 * q]);
+      }
+      if constexpr (BF16) {  // 16 rows x 2 pieces: lanes 0..31
+        bf16_t* dst = EPI == KW_EPI_RESID ? p.hb : reinterpret_cast<bf16_t*>(p.C);
+        const int64_t ld = EPI == KW_EPI_RESID ? p.ldh : p.ldc;
+        const int ml = lane >> 1, q = lane & 1, m = 16 * hj + ml;
+        if (lane < 32 && m < M && nb + 8 * q < p.N) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(&stg[wave][ml][8 * q]);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(&stg[wave][ml][8 * q + 4]);
+          *reinterpret_cast<u32x4*>(dst + (int64_t)m * ld + nb + 8 * q) =
+              u32x4{pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(b[0], b[1]), pack_bf16x2(b[2], b[3])};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = 16 * hj + 4 * (lane >> 4) + r;
+        if (n >= p.N || m >= M) continue;
+        if constexpr (EPI == KW_EPI_RESID) {
+          p.h[(int64_t)m * p.ldh + n] = v4[r];
+          p.hb[(int64_t)m * p.ldh + n] = f2bf(v4[r]);
+        } else {
+          TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v4[r]);
+        }
+      }
+    }
+    KW_DEC_STAMP(4);
+    KW_DEC_STAMP_FLUSH
+    return;
+  }
   if (nw > 1) {
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {

@@ -413,7 +413,7 @@ def _c4_outputs(res, n_rows, P, gc):
     return toks, margin, passes, segs
 
 
-def large_config4_hipmel_fixtures(features_npz, bf16=True):
+def large_config4_hipmel_fixtures(features_npz, bf16=True, seed=0, name="large_v3_c4_hipmel"):
     """tests/golden/large_v3_c4_hipmel.npz: config 4's multi-pass case on the PRODUCT's own inputs (VERDICT r4 item
     1).  ``features_npz`` is tools/dump_hipmel.py's output from the GPU box: the exact f32 log-mel that the HIP feature
     extractor gives stand-in clips 1 and 522 (three seek passes in the fp32 engine, profiles/r04c_multipass_find.json)
@@ -421,11 +421,15 @@ def large_config4_hipmel_fixtures(features_npz, bf16=True):
     settings (run_pseudo_labelling.py:99-102,268,338; max_length 128 with the cumulative growth
     generation_whisper.py:1935-1940): tokens, per-token margins, seek passes per row, segments, and every pass's
     sequence / seek / margins (PassRecorder).  With ``bf16`` the same HF model cast to bfloat16 (the reference's own
-    teacher precision, :229,338) also decodes them: its tokens and passes."""
+    teacher precision, :229,338) also decodes them: its tokens and passes.
+
+    r06: ``seed`` selects another model of the numpy recipe -- seed 6 is the first whose
+    fp32 engine decodes short (zero-padded) stand-in clips in two seek passes (tools/find_multipass.py --seed 6,
+    profiles/r06f_multipass_fp32_seed6.json) -- written as tests/golden/<name>.npz."""
     t0 = time.time()
     z = np.load(features_npz)
     feats = torch.from_numpy(z["features"].astype(np.float32))
-    m = hf_model(LARGE_V3)
+    m = hf_model(LARGE_V3, seed)
     m.generation_config, gc = hf_gen_config(LARGE_V3)
     kw = dict(language="ja", task="transcribe", return_timestamps=True, max_length=128)
     rec = PassRecorder(m)
@@ -433,7 +437,7 @@ def large_config4_hipmel_fixtures(features_npz, bf16=True):
     rec.close()
     P = 3
     toks, margin, passes, segs = _c4_outputs(res, feats.shape[0], P, gc)
-    print(f"  large_v3_c4_hipmel: fp32 generate ({time.time() - t0:.1f}s), passes {passes.tolist()}")
+    print(f"  {name}: fp32 generate ({time.time() - t0:.1f}s), passes {passes.tolist()}")
     out = {"clip_ids": z["clip_ids"], "durations": z["durations"], "features": z["features"].astype(np.float32),
            "tokens": toks, "margin": margin, "passes": passes, "segments": np.array(json.dumps(segs)),
            "max_length": 128, **rec.arrays(P)}
@@ -445,9 +449,10 @@ def large_config4_hipmel_fixtures(features_npz, bf16=True):
         r16.close()
         out["bf16_tokens"] = t16["sequences"].numpy().astype(np.int64)
         out["bf16_passes"] = np.bincount([r for it in r16.iters for r in it["rows"]], minlength=feats.shape[0])
-        print(f"  large_v3_c4_hipmel: bf16 generate ({time.time() - t0:.1f}s), passes {out['bf16_passes'].tolist()}")
-    np.savez_compressed(os.path.join(GOLD, "large_v3_c4_hipmel.npz"), **out)
-    print(f"large_v3_c4_hipmel fixtures done in {time.time() - t0:.1f}s {toks.shape}")
+        print(f"  {name}: bf16 generate ({time.time() - t0:.1f}s), passes {out['bf16_passes'].tolist()}")
+    out["seed"] = np.int64(seed)
+    np.savez_compressed(os.path.join(GOLD, f"{name}.npz"), **out)
+    print(f"{name} fixtures done in {time.time() - t0:.1f}s {toks.shape}")
 
 
 def large_config4_traj_fixtures(traj_npz):
@@ -681,6 +686,7 @@ def main():
     ap.add_argument("--hipmel", default="gpurun_out/c4_hipmel_features.npz",
                     help="--only c4_hipmel: tools/dump_hipmel.py output (the box's HIP log-mel of the chosen clips)")
     ap.add_argument("--no-bf16", action="store_true", help="--only c4_hipmel: skip the bf16 reference run")
+    ap.add_argument("--seed", type=int, default=6, help="--only c4_seed: the numpy recipe's seed of the model")
     ap.add_argument("--traj", default="gpurun_out/c4_traj.npz",
                     help="--only c4_traj: tools/dump_trajectory.py output (the engine's seek passes on the fixture)")
     a = ap.parse_args()
@@ -725,6 +731,8 @@ def main():
         large_longform_fixtures("large_v3_longform8_fp32", LARGE_LONG8_CLIPS)
     if not a.skip_large and a.only == "c4_hipmel":
         large_config4_hipmel_fixtures(a.hipmel, bf16=not a.no_bf16)
+    if not a.skip_large and a.only == "c4_seed":  # r06: tests/golden/large_v3_c4_seed<seed>.npz
+        large_config4_hipmel_fixtures(a.hipmel, bf16=not a.no_bf16, seed=a.seed, name=f"large_v3_c4_seed{a.seed}")
     if not a.skip_large and a.only == "c4_traj":
         large_config4_traj_fixtures(a.traj)
     if not a.skip_large and a.only in (None, "kotoba_beam"):
