@@ -125,41 +125,43 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
     red[v][1][lane] = c1;
   }
   __syncthreads();
-  if (wave != 0) return;
-  f32x4 c0 = red[0][0][lane], c1 = red[0][1][lane];
-  for (int v = 1; v < nv; ++v) {
-    c0 += red[v][0][lane];
-    c1 += red[v][1][lane];
-  }
-  if (lane < 32) {
+  // r06: the two row halves' reduction, LayerNorm statistics and publish on waves 0 and 1 at once (each sums its half's
+  // partial tiles in virtual-wave order and forms its rows' statistics itself: bitwise wave 0 alone doing both, as
+  // kw_dec_linear's spread epilogue)
+  if (wave >= 2) return;
+  const int hh = wave;
+  f32x4 c = red[0][hh][lane];
+  for (int v = 1; v < nv; ++v) c += red[v][hh][lane];
+  if (lane < 16) {
+    const int m = 16 * hh + lane;
     float sx = 0.f, sq = 0.f;
     for (int v = 0; v < nv; ++v) {
-      sx += rpart[v][lane][0];
-      sq += rpart[v][lane][1];
+      sx += rpart[v][m][0];
+      sq += rpart[v][m][1];
     }
     const float inv = 1.f / (float)a.K;
     const float mean = sx * inv;
-    rstat[lane][0] = mean;
-    rstat[lane][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + a.ln_eps);
+    rstat[m][0] = mean;
+    rstat[m][1] = rsqrtf(fmaxf(sq * inv - mean * mean, 0.f) + a.ln_eps);
   }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   const int n = cg * 16 + (lane & 15);
   const bool drop = cg == 0 && fault != 0;  // test hook: this launch's consumers of columns [0, 16) time out
-  if (drop && lane == 0) __hip_atomic_store(a.fault, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (drop && wave == 0 && lane == 0) __hip_atomic_store(a.fault, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = 16 * hh + 4 * (lane >> 4) + r;
-      float v = hh ? c1[r] : c0[r];
-      v = rstat[m][1] * (v - rstat[m][0] * ecsum);
-      v += ebias;
-      if (n < a.scale_cols) v *= a.scale;
-      const uint32_t mine = f2bf(v);
-      const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, false);  // lane ^ 1
-      if ((lane & 1) == 0 && m < M && n < a.N && !drop)
-        __hip_atomic_store(gran + (int64_t)m * (a.N / 2) + (n >> 1), (1ull << 32) | (mine | (other << 16)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+  for (int r = 0; r < 4; ++r) {
+    const int m = 16 * hh + 4 * (lane >> 4) + r;
+    float v = c[r];
+    v = rstat[m][1] * (v - rstat[m][0] * ecsum);
+    v += ebias;
+    if (n < a.scale_cols) v *= a.scale;
+    const uint32_t mine = f2bf(v);
+    const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)mine, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+    if ((lane & 1) == 0 && m < M && n < a.N && !drop)
+      __hip_atomic_store(gran + (int64_t)m * (a.N / 2) + (n >> 1), (1ull << 32) | (mine | (other << 16)),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
