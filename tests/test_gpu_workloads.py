@@ -44,11 +44,11 @@ def _gpu():
         pytest.skip("no GPU")
 
 
-def _model(shape, dtype, pad=None):
+def _model(shape, dtype, pad=None, seed=0):
     from kwhisper.generation import KWhisperForConditionalGeneration
 
     return KWhisperForConditionalGeneration.from_state_dict(
-        shape, synthetic_state_dict(shape, 0), dtype=dtype, generation_config=generation_constants(shape, pad))
+        shape, synthetic_state_dict(shape, seed), dtype=dtype, generation_config=generation_constants(shape, pad))
 
 
 def _free():
@@ -698,6 +698,43 @@ def test_config4_hipmel_multipass(gold):
           f"{sum(np.array_equal(a, b) for a, b in zip(t16, g['tokens']))}/{n}")
     assert len(bad) == 0, f"(pass entry, step) pairs whose safe-margin greedy choice differs: {bad[:8]}"
     assert n_cmp >= 0.9 * n_tot
+    del m16
+    _free()
+
+
+def test_config4_seed6_short_clip_multipass(gold):
+    """Config 4's seek advance INSIDE a zero-padded short clip at large-v3.  The fixture model
+    (the numpy recipe's seed 0) takes one pass on all 1,768 stand-in clips, and so do seeds 1 (fp32 engine) and 2-5, 7-9
+    (bf16 engine; profiles/r06d_*, r06e_multipass_scan_bf16.json); seed 6 takes two on 8 of the first batch's 32 clips, in the bf16 and in the fp32 engine (tools/find_multipass.py --seed
+    6, profiles/r06f_multipass_fp32_seed6.json).  tests/golden/large_v3_c4_seed6.npz holds the HIP log-mel of 14 of
+    them (8 multi-pass) from the GPU box and transformers' fp32 / bf16 large-v3 of seed 6 on exactly those features
+    (tools/make_fixtures.py --only c4_seed --seed 6; run_pseudo_labelling.py:99-102,268,338): transformers takes two
+    seek passes on the same 8 rows -- the mel re-encoded from the last complete segment's timestamp, the cumulative
+    max_length growth (generation_whisper.py:785-903,1932-1940).  The fp32 engine through pseudo_label() is bit-exact
+    with transformers' fp32 tokens AND per-row passes; the bf16 engine is teacher-forced along every fp32 pass, its
+    safe-margin greedy choice equal to fp32's, passes >= 2 included."""
+    g = gold("large_v3_c4_seed6")
+    assert int(g["seed"]) == 6 and int((g["passes"] >= 2).sum()) >= 8
+    feats = torch.from_numpy(g["features"]).cuda()
+    n = feats.shape[0]
+    m32 = _model(LARGE_V3, torch.float32, seed=6)
+    ids, preds = _c4_pseudo_label(m32, g["durations"], feats, n)
+    assert ids == list(range(n))
+    np.testing.assert_array_equal(np.stack(preds), g["tokens"])
+    np.testing.assert_array_equal(m32.stats["row_passes"], g["passes"])
+    print(f"\nconfig4 seed-6 short clips {g['clip_ids'].tolist()}: transformers fp32 seek passes {g['passes'].tolist()} "
+          f"(bf16 reference {g['bf16_passes'].tolist()}); fp32 engine bit-exact, same passes")
+    del m32
+    _free()
+    m16 = _model(LARGE_V3, torch.bfloat16, seed=6)
+    n_cmp, n_tot, n_cmp2, n_tot2, bad = _teacher_forced_per_pass(m16, feats, g)
+    t16 = m16.generate(feats, **C4_KW).cpu().numpy()
+    print(f"config4 seed-6 bf16 teacher-forced per pass: {n_cmp} of {n_tot} steps compared (margin >= {MARGIN_FLOOR}; "
+          f"passes >= 2: {n_cmp2} of {n_tot2}), {len(bad)} differ; free-running bf16 passes "
+          f"{m16.stats['row_passes'].tolist()}, rows identical to fp32 "
+          f"{sum(np.array_equal(a, b) for a, b in zip(t16, g['tokens']))}/{n}")
+    assert len(bad) == 0, f"(pass entry, step) pairs whose safe-margin greedy choice differs: {bad[:8]}"
+    assert n_cmp >= 0.9 * n_tot and n_cmp2 > 0
     del m16
     _free()
 
