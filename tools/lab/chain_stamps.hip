@@ -44,6 +44,35 @@ struct Shape {
   int N, K, resid, ln, gelu, bf16out;
 };
 
+// fc2 geometry variants through the production kernels with a chosen Geo (ks K-splits of nw waves x ktm k-tiles)
+static float fc2_geo(const char* name, int ktm, int nw, int ks, hipStream_t s, bf16_t* x, float* h, bf16_t* hb, float* bias,
+                     void* ws, std::vector<void*>& Ws) {
+  const int M = 32, N = 1280, K = 5120, L = (int)Ws.size();
+  DecP p{};
+  p.x = x; p.ldx = K; p.ln = 0; p.ln_eps = 1e-5f; p.W = nullptr; p.bias = bias; p.C = nullptr; p.ldc = N;
+  p.gelu = 0; p.scale = 1.f; p.scale_cols = 0; p.h = h; p.hb = hb; p.ldh = N; p.M = M; p.N = N; p.K = K;
+  p.cnt = reinterpret_cast<int*>(ws); p.slab = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + CNT_MAX * sizeof(int));
+  p.xlds = 1; p.vec_epi = 1;
+  Geo g{1, ktm, nw, ks};
+  hipGraph_t gr; hipGraphExec_t ge;
+  CK(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+  for (int i = 0; i < L; ++i) {
+    p.W = reinterpret_cast<const bf16x8*>(Ws[i]);
+    CK(launch(p, true, g, true, s));
+  }
+  CK(hipStreamEndCapture(s, &gr));
+  CK(hipGraphInstantiate(&ge, gr, nullptr, nullptr, 0));
+  for (int i = 0; i < 3; ++i) CK(hipGraphLaunch(ge, s));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  CK(hipEventRecord(e0, s));
+  for (int i = 0; i < 20; ++i) CK(hipGraphLaunch(ge, s));
+  CK(hipEventRecord(e1, s)); CK(hipEventSynchronize(e1));
+  float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+  printf("%-40s %6.2f us/launch\n", name, ms * 1000.f / (20 * L));
+  CK(hipGraphExecDestroy(ge)); CK(hipGraphDestroy(gr));
+  return ms;
+}
+
 int main() {
   hipStream_t s;
   CK(hipStreamCreate(&s));
@@ -60,6 +89,19 @@ int main() {
   float* cs; CK(hipMalloc(&cs, 5120 * 4)); CK(hipMemset(cs, 0, 5120 * 4));
   void* ws; CK(hipMalloc(&ws, 32 << 20)); CK(hipMemset(ws, 0, 32 << 20));
   std::vector<unsigned long long> st(2048 * 8);
+  if (getenv("FC2_GEO")) {  // fc2 K-split geometry sweep, then exit
+    std::vector<void*> Ws(L);
+    for (int i = 0; i < L; ++i) { CK(hipMalloc(&Ws[i], (size_t)1280 * 5120 * 2)); CK(hipMemset(Ws[i], 0x3c, (size_t)1280 * 5120 * 2)); }
+    for (int rep = 0; rep < 2; ++rep) {
+      fc2_geo("fc2 ks 6 x 6 waves x 5 (product)", 5, 6, 6, s, x, h, hb, bias, ws, Ws);
+      fc2_geo("fc2 ks 4 x 8 waves x 5", 5, 8, 4, s, x, h, hb, bias, ws, Ws);
+      fc2_geo("fc2 ks 3 x 6 waves x 10", 10, 6, 3, s, x, h, hb, bias, ws, Ws);
+      fc2_geo("fc2 ks 4 x 4 waves x 10", 10, 4, 4, s, x, h, hb, bias, ws, Ws);
+      fc2_geo("fc2 ks 8 x 4 waves x 5", 5, 4, 8, s, x, h, hb, bias, ws, Ws);
+      fc2_geo("fc2 ks 5 x 8 waves x 4(5)", 5, 8, 5, s, x, h, hb, bias, ws, Ws);
+    }
+    return 0;
+  }
   for (const Shape& sh : shapes) {
     std::vector<void*> Ws(L);
     for (int i = 0; i < L; ++i) {
