@@ -72,6 +72,55 @@ struct DecP {
   int vec_epi;  // outputs in whole 16-B pieces (N % 16 == 0, 16-B aligned rows): the epilogue stores 16-B pieces
 };
 
+// One wave's 16 x 16 output block: lane holds rows mb + 4 (lane / 16) + r (r < 4) of column nb + lane % 16 (the MFMA C
+// layout).  vec (DecP::vec_epi): staged row-major in stg (the wave's own 16 x 20 floats of LDS) and stored as whole
+// 16-B pieces -- f32 rows of 4 columns (one per lane), bf16 rows of 8 (lanes 0..31) -- otherwise element by element;
+// rows >= M and columns >= N are not stored.  RESID: h (f32) and its bf16 mirror hb; STORE: C of TC.  r06: the
+// element stores wrote 16 columns x 4 rows of 2-4-B pieces per instruction.
+template <int EPI, typename TC>
+__device__ __forceinline__ void store_block16(const DecP& p, float (*stg)[20], const float (&v4)[4], int mb, int M,
+                                              int nb, int lane) {
+  if (p.vec_epi) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) stg[4 * (lane >> 4) + r][lane & 15] = v4[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    constexpr bool F32 = EPI == KW_EPI_RESID || sizeof(TC) == 4, BF16 = EPI == KW_EPI_RESID || sizeof(TC) == 2;
+    if constexpr (F32) {
+      float* dst = EPI == KW_EPI_RESID ? p.h : reinterpret_cast<float*>(p.C);
+      const int64_t ld = EPI == KW_EPI_RESID ? p.ldh : p.ldc;
+      const int ml = lane >> 2, q = lane & 3, m = mb + ml;
+      if (m < M && nb + 4 * q < p.N)
+        *reinterpret_cast<f32x4*>(dst + (int64_t)m * ld + nb + 4 * q) = *reinterpret_cast<const f32x4*>(&stg[ml][4 * q]);
+    }
+    if constexpr (BF16) {
+      bf16_t* dst = EPI == KW_EPI_RESID ? p.hb : reinterpret_cast<bf16_t*>(p.C);
+      const int64_t ld = EPI == KW_EPI_RESID ? p.ldh : p.ldc;
+      const int ml = lane >> 1, q = lane & 1, m = mb + ml;
+      if (lane < 32 && m < M && nb + 8 * q < p.N) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&stg[ml][8 * q]);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(&stg[ml][8 * q + 4]);
+        *reinterpret_cast<u32x4*>(dst + (int64_t)m * ld + nb + 8 * q) =
+            u32x4{pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(b[0], b[1]), pack_bf16x2(b[2], b[3])};
+      }
+    }
+  } else {
+    const int n = nb + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = mb + 4 * (lane >> 4) + r;
+      if (n >= p.N || m >= M) continue;
+      if constexpr (EPI == KW_EPI_RESID) {
+        p.h[(int64_t)m * p.ldh + n] = v4[r];
+        p.hb[(int64_t)m * p.ldh + n] = f2bf(v4[r]);
+      } else {
+        TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v4[r]);
+      }
+    }
+  }
+}
+
 // H2: the second 16-row half of the tile exists (false: a row-split chunk of <= 16 rows -- its a1 / c1 / LayerNorm
 // statistics are never loaded or computed, which frees the registers for two workgroups per CU)
 template <int KTM, int NCB, bool LNA, int EPI, typename TC, bool H2 = true>
@@ -291,44 +340,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
       }
       v4[r] = v;
     }
-    if (p.vec_epi) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) stg[wave][4 * (lane >> 4) + r][lane & 15] = v4[r];
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      constexpr bool F32 = EPI == KW_EPI_RESID || sizeof(TC) == 4, BF16 = EPI == KW_EPI_RESID || sizeof(TC) == 2;
-      if constexpr (F32) {  // 16 rows x 4 pieces: one per lane
-        float* dst = EPI == KW_EPI_RESID ? p.h : reinterpret_cast<float*>(p.C);
-        const int64_t ld = EPI == KW_EPI_RESID ? p.ldh : p.ldc;
-        const int ml = lane >> 2, q = lane & 3, m = 16 * hj + ml;
-        if (m < M && nb + 4 * q < p.N)
-          *reinterpret_cast<f32x4*>(dst + (int64_t)m * ld + nb + 4 * q) = *reinterpret_cast<const f32x4*>(&stg[wave][ml][4 * q]);
-      }
-      if constexpr (BF16) {  // 16 rows x 2 pieces: lanes 0..31
-        bf16_t* dst = EPI == KW_EPI_RESID ? p.hb : reinterpret_cast<bf16_t*>(p.C);
-        const int64_t ld = EPI == KW_EPI_RESID ? p.ldh : p.ldc;
-        const int ml = lane >> 1, q = lane & 1, m = 16 * hj + ml;
-        if (lane < 32 && m < M && nb + 8 * q < p.N) {
-          const f32x4 a = *reinterpret_cast<const f32x4*>(&stg[wave][ml][8 * q]);
-          const f32x4 b = *reinterpret_cast<const f32x4*>(&stg[wave][ml][8 * q + 4]);
-          *reinterpret_cast<u32x4*>(dst + (int64_t)m * ld + nb + 8 * q) =
-              u32x4{pack_bf16x2(a[0], a[1]), pack_bf16x2(a[2], a[3]), pack_bf16x2(b[0], b[1]), pack_bf16x2(b[2], b[3])};
-        }
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = 16 * hj + 4 * (lane >> 4) + r;
-        if (n >= p.N || m >= M) continue;
-        if constexpr (EPI == KW_EPI_RESID) {
-          p.h[(int64_t)m * p.ldh + n] = v4[r];
-          p.hb[(int64_t)m * p.ldh + n] = f2bf(v4[r]);
-        } else {
-          TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)m * p.ldc + n, v4[r]);
-        }
-      }
-    }
+    store_block16<EPI, TC>(p, stg[wave], v4, 16 * hj, M, nb, lane);
     KW_DEC_STAMP(4);
     KW_DEC_STAMP_FLUSH
     return;
@@ -530,6 +542,7 @@ __global__ __launch_bounds__(512) void dec_linear_kernel(DecP p0, int ksn) {
 template <int KTM, int NCB, bool LNA, int EPI, typename TC>
 __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) {
   __shared__ f32x4 red[MAXW][NCB][2][64];
+  __shared__ __attribute__((aligned(16))) float stg[MAXW][16][20];  // store_block16's staging, one block per wave
   __shared__ float rpart[MAXW][32][2];
   __shared__ float rstat[32][2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
@@ -675,28 +688,24 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
         f32x4 acc = red[0][c][hh][lane];
         for (int w2 = 1; w2 < nw; ++w2) acc += red[w2][c][hh][lane];
         const int n = (cg * NCB + c) * 16 + (lane & 15);
-        const bool nvalid = n < p.N;
         const float bn = ebias[c];
         const float cs = ecsum[c];
+        float v4[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = 16 * hh + 4 * (lane >> 4) + r;
-          const bool valid = nvalid && m < M;
           float v = acc[r];
           if constexpr (LNA) v = rstat[m][1] * (v - rstat[m][0] * cs);
           v += bn;
           if constexpr (EPI == KW_EPI_RESID) {
             v += hold[c][hh][r];
-            if (valid) {
-              p.h[(int64_t)(m0 + m) * p.ldh + n] = v;
-              p.hb[(int64_t)(m0 + m) * p.ldh + n] = f2bf(v);
-            }
           } else {
             if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
             if (n < p.scale_cols) v *= p.scale;
-            if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)(m0 + m) * p.ldc + n, v);
           }
+          v4[r] = v;
         }
+        store_block16<EPI, TC>(p, stg[wave], v4, m0 + 16 * hh, m0 + M, (cg * NCB + c) * 16, lane);
       }
     } else if (wave == 0) {
       for (int w2 = 1; w2 < nw; ++w2)
@@ -721,34 +730,30 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
 #pragma unroll
       for (int c = 0; c < NCB; ++c) {
         const int n = (cg * NCB + c) * 16 + (lane & 15);
-        const bool nvalid = n < p.N;
         const float bn = ebias[c];
         const float cs = ecsum[c];
 #pragma unroll
         for (int hh = 0; hh < 2; ++hh) {
+          float v4[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int m = 16 * hh + 4 * (lane >> 4) + r;
-            const bool valid = nvalid && m < M;
             float v = hh ? c1[c][r] : c0[c][r];
             if constexpr (LNA) v = rstat[m][1] * (v - rstat[m][0] * cs);
             v += bn;
             if constexpr (EPI == KW_EPI_RESID) {
               v += hold[c][hh][r];
-              if (valid) {
-                p.h[(int64_t)(m0 + m) * p.ldh + n] = v;
-                p.hb[(int64_t)(m0 + m) * p.ldh + n] = f2bf(v);
-              }
             } else {
               if (p.gelu) v = sizeof(TC) == 2 ? gelu_bf16out(v) : gelu_erf(v);
               if (n < p.scale_cols) v *= p.scale;
-              if (valid) TypeIO<TC>::st(reinterpret_cast<TC*>(p.C) + (int64_t)(m0 + m) * p.ldc + n, v);
             }
+            v4[r] = v;
           }
+          store_block16<EPI, TC>(p, stg[0], v4, m0 + 16 * hh, m0 + M, (cg * NCB + c) * 16, lane);
         }
       }
     }
-    __syncthreads();  // red / rpart / rstat are rewritten by the next chunk
+    __syncthreads();  // red / rpart / rstat / stg are rewritten by the next chunk
   }
 }
 

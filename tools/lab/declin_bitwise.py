@@ -30,7 +30,7 @@ def dump(path):
         cs = ops.ln_colsum(W)
         b = torch.randn(N, device="cuda", generator=g) * 0.1
         ws = torch.zeros(ops.dec_linear_workspace_bytes(N, K) // 4 + 1, device="cuda")
-        for M in (1, 5, 16, 17, 32):
+        for M in (1, 5, 16, 17, 32, 64, 70, 128, 320):
             x = (torch.randn(M, K, device="cuda", generator=g) * 2 + 0.3).bfloat16()
             if mode == "resid":
                 h = torch.randn(M, N, device="cuda", generator=g)
