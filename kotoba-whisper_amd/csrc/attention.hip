@@ -1170,19 +1170,25 @@ struct CRP {
   ProjArgs proj;  // QG: the query projection
 };
 
-__device__ __forceinline__ void row_issue(const bf16_t* base, int k0, int k1, int slot, int sub, u32x4 (&r)[8]) {
+// a chunk's 16-B pieces of the pair's K or V rows (lane: row k0 + slot + 32 j, bytes voff = (slot * 64 + sub * 8) * 2
+// of it) through a buffer resource over the pair's S rows: rows past S read as 0 (masked like every row past the
+// chunk end), so no per-piece clamp or 64-bit address arithmetic -- one add per piece
+__device__ __forceinline__ void row_issue(__amdgpu_buffer_rsrc_t rs, int k0, uint32_t voff, u32x4 (&r)[8]) {
   __builtin_amdgcn_sched_barrier(0);  // issue exactly here: the schedule is the point (the compiler would sink these
 #pragma unroll                        // loads below the next chunk's arithmetic and wait on them there)
-  for (int j = 0; j < 8; ++j) r[j] = ld_row8<bf16_t>(base + (int64_t)min(k0 + slot + 32 * j, k1 - 1) * HD + sub * 8).u[0];
+  for (int j = 0; j < 8; ++j)
+    r[j] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff + (uint32_t)((k0 + 32 * j) * HD * 2), 0, 2));
   __builtin_amdgcn_sched_barrier(0);
 }
 
 // one chunk of the pair: its scores from K (then the caller's next V load goes out, the K registers being dead),
-// its values from V, merged into the wave's running (M, Lr, A)
+// its values from V, merged into the wave's running (M, Lr, A).  Every chunk holds more than 224 keys (the host's
+// row_kernel_fits), so only key group j = 7 can fall past the chunk end.
+constexpr int ROW_JV = 7;
 __device__ __forceinline__ void row_fold(float mw, const float (&sc)[8], const u32x4 (&vr)[8], int k0, int k1, int slot,
                                          float& M, float& Lr, float (&A)[8]) {
   float lw, acc[8], f0 = 0.f, f1 = 0.f;
-  wave_values_bf16(sc, mw, vr, k0, k1, slot, 8, lw, acc);
+  wave_values_bf16<32, ROW_JV>(sc, mw, vr, k0, k1, slot, 8, lw, acc);
   const int mode = fold_begin(mw, lw, M, Lr, f0, f1);
 #pragma unroll
   for (int i = 0; i < 8; ++i) A[i] = fold_value(mode, A[i], acc[i], f0, f1);
@@ -1217,13 +1223,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   }
   constexpr int ns = NS;
   const int chunk = p.chunk, S = p.S;
+  const __amdgpu_buffer_rsrc_t rsk = __builtin_amdgcn_make_buffer_rsrc((void*)kb, (short)0, S * HD * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsv = __builtin_amdgcn_make_buffer_rsrc((void*)vb, (short)0, S * HD * 2, 0x00020000);
+  const uint32_t voff = (uint32_t)((slot * HD + sub * 8) * 2);
   // three 32-register K / V sets in rotation: chunk c + 1's K goes out before chunk c's scores, its V right
   // after them (into chunk c's dead K registers), chunk c + 2's K after chunk c's values (into its dead V
   // registers) -- one chunk in flight while one is computed, 96 K / V registers live
   u32x4 r0[8], r1[8], r2[8];
-  row_issue(kb, 0, min(S, chunk), slot, sub, r0);
-  row_issue(vb, 0, min(S, chunk), slot, sub, r1);
-  if (ns > 1) row_issue(kb, chunk, min(S, 2 * chunk), slot, sub, r2);
+  row_issue(rsk, 0, voff, r0);
+  row_issue(rsv, 0, voff, r1);
+  if (ns > 1) row_issue(rsk, chunk, voff, r2);
   if constexpr (QG) {
     bool ok = ((g[0] & g[1] & g[2] & g[3]) >> 32) == 1ull;
     for (int it = 0; __builtin_amdgcn_ballot_w64(!ok) != 0; ++it) {  // the projection not yet published: poll
@@ -1259,10 +1268,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   auto step = [&](const int c, u32x4 (&rk)[8], u32x4 (&rv)[8]) __attribute__((always_inline)) {
     float sc[8];
     const int k0 = c * chunk, k1 = min(S, k0 + chunk);
-    const float mw = wave_scores_bf16(ql, rk, k0, k1, slot, 8, sc);
-    if (c + 1 < ns) row_issue(vb, k1, min(S, k1 + chunk), slot, sub, rk);
+    const float mw = wave_scores_bf16<32, ROW_JV>(ql, rk, k0, k1, slot, 8, sc);
+    if (c + 1 < ns) row_issue(rsv, k1, voff, rk);
     row_fold(mw, sc, rv, k0, k1, slot, M, Lr, A);
-    if (c + 2 < ns) row_issue(kb, k0 + 2 * chunk, min(S, k0 + 3 * chunk), slot, sub, rv);
+    if (c + 2 < ns) row_issue(rsk, k0 + 2 * chunk, voff, rv);
   };
 #pragma unroll
   for (int c = 0; c < ns; c += 3) {
@@ -1808,7 +1817,10 @@ extern "C" size_t kw_cross_attn_status_offset(int64_t B, int64_t q_len, int64_t 
 constexpr int ROW_NS = 6;  // cross_attn_row_kernel's chunk count (S = 1500)
 
 template <bool QG>
-static bool row_kernel_fits(int64_t rows, int ns) {
+static bool row_kernel_fits(int64_t rows, int64_t S) {
+  const int ns = cross_splits(S);
+  const int64_t chunk = (S + ns - 1) / ns;
+  if (chunk <= 32 * ROW_JV || S - (int64_t)(ns - 1) * chunk <= 32 * ROW_JV) return false;  // row_fold's key groups
   static int ncu = 0, per_cu = 0, off = -1;
   if (off < 0) {
     const char* e = getenv("KW_CROSS_ROW");
@@ -1823,8 +1835,7 @@ static bool row_kernel_fits(int64_t rows, int ns) {
 }
 
 extern "C" int kw_cross_attn_pair_kernel(int64_t rows, int64_t S, int fused) {
-  const int ns = cross_splits(S);
-  return (fused ? row_kernel_fits<true>(rows, ns) : row_kernel_fits<false>(rows, ns)) ? 1 : 0;
+  return (fused ? row_kernel_fits<true>(rows, S) : row_kernel_fits<false>(rows, S)) ? 1 : 0;
 }
 
 extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q_len, int64_t H, int64_t hd,
@@ -1861,7 +1872,7 @@ extern "C" int kw_cross_attn_step(int dtype, const void* q, int64_t B, int64_t q
     const dim3 gm((unsigned)(B * ((q_len + 7) / 8) * H), (unsigned)ns);
     hipLaunchKernelGGL((cross_attn_multi_kernel<bf16_t, 8>), gm, dim3(256), 0, s, (const bf16_t*)q, (int)q_len, (int)H,
                        (const bf16_t*)k, (const bf16_t*)v, (int)S, chunk, part, cnt, (bf16_t*)out);
-  } else if (dtype == KW_DT_BF16 && q_len == 1 && row_kernel_fits<false>(B * H, ns)) {
+  } else if (dtype == KW_DT_BF16 && q_len == 1 && row_kernel_fits<false>(B * H, S)) {
     CRP p{};
     p.q = (const bf16_t*)q;
     p.kc = (const bf16_t*)k;
@@ -1940,7 +1951,7 @@ extern "C" int kw_dec_xq_cross(const kw_dec_xq_cross_args* a, kw_stream_t stream
   p.gran = reinterpret_cast<unsigned long long*>(ws + cross_granule_offset(a->M, 1, a->H, a->S));
   p.err = reinterpret_cast<int*>(ws + cross_partials_bytes(a->M, 1, a->H, a->S)) + a->M * a->H;
   p.out = reinterpret_cast<bf16_t*>(a->out);
-  if (row_kernel_fits<true>(a->M * a->H, p.ns)) {  // one pair workgroup per (row, head), chunks pipelined
+  if (row_kernel_fits<true>(a->M * a->H, a->S)) {  // one pair workgroup per (row, head), chunks pipelined
     CRP r{};
     r.qg = p.qg;
     r.kc = p.kc;

@@ -46,7 +46,9 @@ __device__ __forceinline__ void unpack8(const Row8<T>& r, float v[8]) {
 // an explicit fmaf so every kernel that uses these helpers rounds identically (bitwise-equal rows).
 // the two halves of wave_row_bf16, for kernels that interleave loads between them: the scores (log2 units)
 // and the wave maximum ...
-template <int KS = 32>  // key of (slot, j) = k0 + slot + KS * j (32 key slots per 4-wave row, 16 per 2-wave row)
+// JV: the first key group j that can fall past the chunk end (a caller whose chunks all hold more than KS * (JV - 1)
+// keys passes JV > 0 and the groups below it skip the check; the arithmetic is the same)
+template <int KS = 32, int JV = 0>  // key of (slot, j) = k0 + slot + KS * j (32 key slots per 4-wave row, 16 per 2-wave row)
 __device__ __forceinline__ float wave_scores_bf16(const float ql[8], const u32x4 kr[8], int k0, int k1, int slot,
                                                   int nj, float sc[8]) {
   float mx = -INFINITY;
@@ -62,7 +64,7 @@ __device__ __forceinline__ float wave_scores_bf16(const float ql[8], const u32x4
         sj = fmaf(ql[2 * i + 1], __uint_as_float(w[i] & 0xffff0000u), sj);
       }
       sj = kw_sum8(sj);
-      sc[j] = (k0 + slot + KS * j < k1) ? sj : -INFINITY;
+      sc[j] = (j < JV || k0 + slot + KS * j < k1) ? sj : -INFINITY;
       mx = fmaxf(mx, sc[j]);
     }
   }
@@ -70,7 +72,7 @@ __device__ __forceinline__ float wave_scores_bf16(const float ql[8], const u32x4
 }
 
 // ... then p = exp2(s - m_w), the row sum and this lane's 8 value dims reduced over the wave's key slots
-template <int KS = 32>
+template <int KS = 32, int JV = 0>
 __device__ __forceinline__ void wave_values_bf16(const float sc[8], float mx, const u32x4 vr[8], int k0, int k1,
                                                  int slot, int nj, float& lw, float acc[8]) {
   float lsum = 0.f;
@@ -79,7 +81,7 @@ __device__ __forceinline__ void wave_values_bf16(const float sc[8], float mx, co
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (j < nj) {
-      const bool valid = k0 + slot + KS * j < k1;
+      const bool valid = j < JV || k0 + slot + KS * j < k1;
       const float pj = valid ? __builtin_amdgcn_exp2f(sc[j] - mx) : 0.f;
       lsum += pj;
       // a masked slot holds a clamped row that may be STALE (a cache row this step has not written yet, e.g. the
