@@ -1189,7 +1189,12 @@ __device__ __forceinline__ void row_fold(float mw, const float (&sc)[8], const u
                                          float& M, float& Lr, float (&A)[8]) {
   float lw, acc[8], f0 = 0.f, f1 = 0.f;
   wave_values_bf16<32, ROW_JV>(sc, mw, vr, k0, k1, slot, 8, lw, acc);
-  const int mode = fold_begin(mw, lw, M, Lr, f0, f1);
+  // m_w and l_w come out of full-wave butterflies (commutative adds / maxima: every lane holds the same bits), so
+  // lane 0's copy IS the value: read as scalars, (M, Lr) and the fold mode are scalar and the fold is a scalar
+  // branch, not eight exec-masked ones per chunk
+  const float mu = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, mw)));
+  const float lu = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, lw)));
+  const int mode = fold_begin(mu, lu, M, Lr, f0, f1);
 #pragma unroll
   for (int i = 0; i < 8; ++i) A[i] = fold_value(mode, A[i], acc[i], f0, f1);
 }
