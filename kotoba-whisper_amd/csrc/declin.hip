@@ -129,7 +129,7 @@ __device__ __forceinline__ void dec_linear_body(DecP p, const int ksn, const int
   __shared__ float rpart[MAXW][32][2];  // LayerNorm: per-wave row (sum, sum of squares)
   __shared__ float rstat[32][2];     // LayerNorm: (mean, rstd) per row
   extern __shared__ __attribute__((aligned(16))) char xs[];  // activation image (x_lds_bytes)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform (scalar branches)
   const int nkt = p.K >> 5;
   const int nsl = ksn * nw, sl = ks * nw + wave;
   const int kt0 = (nkt * sl) / nsl, kt1 = (nkt * (sl + 1)) / nsl;  // <= KTM k-tiles (host-checked)
@@ -545,7 +545,7 @@ __global__ __launch_bounds__(512) void dec_linear_rows_kernel(DecP p, int zper) 
   __shared__ __attribute__((aligned(16))) float stg[MAXW][16][20];  // store_block16's staging, one block per wave
   __shared__ float rpart[MAXW][32][2];
   __shared__ float rstat[32][2];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   const int cg = blockIdx.x;
   const int nkt = p.K >> 5;
   const int kt0 = (nkt * wave) / nw, kt1 = (nkt * (wave + 1)) / nw;  // <= KTM (host-checked)
@@ -791,7 +791,7 @@ __global__ __launch_bounds__(64 * NWV) void lm_head_rows_kernel(DecP p) {
   static_assert(NZ <= LMR_NZ && 32 * NZ <= 16 * NWV * G && PD > LEAD, "lm_head_rows_kernel geometry");
   __shared__ __attribute__((aligned(16))) char abuf[NBUF][SLICE];
   __shared__ float rsum[LMR_MAXROWS], rsq[LMR_MAXROWS];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform (scalar branches)
   const int M = p.M, nkt = p.K >> 5, nz = (M + 31) / 32;
   const int n_cb = (p.N + 15) / 16;
   const int cb = min(blockIdx.x * NWV + wave, n_cb - 1);
@@ -1059,7 +1059,7 @@ __global__ __launch_bounds__(512) void lm_head_kernel(DecP p0, int groups_per_wg
   // the run's logits, written back after the loop as whole row spans: a group's 16 x 16 tiles stored in place were
   // 4 x 64-B pieces per wave instruction (rows 207 KB apart), 4 us of a 33 us launch (profiles/r05g_lmh_decomposition.txt)
   __shared__ float obuf[32][LMH_MAXG * LMH_NCB * 16 + 1];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6), nw = blockDim.x >> 6;
   const int nkt = p.K >> 5;
   const int kt0 = (nkt * wave) / nw, kt1 = (nkt * (wave + 1)) / nw;  // <= LMH_KTM (host-checked)
   const int ktl = max(kt1 - 1, kt0);

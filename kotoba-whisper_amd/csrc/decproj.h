@@ -44,7 +44,7 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
   f32x4(*red)[2][64] = reinterpret_cast<f32x4(*)[2][64]>(scratch);           // [8][2][64]
   float(*rpart)[32][2] = reinterpret_cast<float(*)[32][2]>(scratch + 16384);  // [8][32][2]
   float(*rstat)[2] = reinterpret_cast<float(*)[2]>(scratch + 16384 + 2048);   // [32][2]
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int M = a.M, nkt = a.K >> 5;
   const int nv = (nkt + PROJ_KTM - 1) / PROJ_KTM;
   const bf16_t* x0 = a.x + (int64_t)min(lane & 15, M - 1) * a.ldx + (lane >> 4) * 8;

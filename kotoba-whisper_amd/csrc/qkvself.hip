@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void q
                           blockIdx.x, scratch, p.gran);
     return;
   }
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform (scalar branches)
   const int ps = wave >> 1, pw = wave & 1, ptid = tid & 127;  // pair slot (2 waves each), wave within it
   const int L = *p.cur_len;  // positions [0, L - 1) cached, L - 1 new
   const bool len_ok = L >= 1 && L <= QS_MAX_LEN && L <= p.t_max;
