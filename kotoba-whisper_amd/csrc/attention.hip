@@ -517,7 +517,7 @@ __global__ __launch_bounds__(256) void attn_fwd_f32(const float* __restrict__ qk
   __shared__ float ks[64][HD + 1];
   __shared__ float vs[64][HD + 1];
   __shared__ float qs[4][HD];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n_qb = (T + 3) / 4;
   const int bh = blockIdx.x / n_qb, qb = blockIdx.x - bh * n_qb;
   const int b = bh / H, h = bh - (bh / H) * H;
@@ -589,7 +589,7 @@ template <typename T, typename KP, typename VP>
 __device__ __forceinline__ void attend_rows(const float qv[8], int k0, int k1, KP kp, VP vp, float* sc,
                                             float (*red)[65], float* stat, float& m_out, float& l_out,
                                             float& o_out) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sub = lane & 7, kslot = wave * 8 + (lane >> 3);
   float mx = -INFINITY;
   // 4 rows per lane group in flight (addresses clamped, results masked: loads stay unconditional)
@@ -655,7 +655,7 @@ __device__ __forceinline__ void attend_rows(const float qv[8], int k0, int k1, K
 template <typename T, typename KP, typename VP>
 __device__ __forceinline__ void attend_chunk(const float qv[8], int k0, int k1, KP kp, VP vp, float (*red)[64],
                                              float* stat, float& m_out, float& l_out, float& o_out) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
   Row8<T> kr[8], vr[8];
   // key groups j past the chunk (k0 + 32j >= k1: workgroup-uniform, e.g. the short self-attention chunks of
@@ -805,7 +805,7 @@ __device__ __forceinline__ void wave_partials_combine(unsigned long long* gr, in
                                                       const float (&acc)[8], float (*red)[64], float* stat,
                                                       bf16_t* out_row, int* err) {
   constexpr int G = HD + 2, NSMAX = 8;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   if (lane < 8) {  // the wave's partial of dim d = lane*8 + i, read back by lane d of the same wave (in order)
 #pragma unroll
     for (int i = 0; i < 8; ++i) red[wave][lane * 8 + i] = acc[i];
@@ -1006,7 +1006,7 @@ __global__ __launch_bounds__(256) void cross_attn_dma_kernel(const bf16_t* __res
   __shared__ float stat[8];
   const int row = blockIdx.x, split = blockIdx.y, ns = gridDim.y;
   const int h = row % H, bq = row / H, b = bq / q_len;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
   const int k0 = split * chunk, k1 = min(S, k0 + chunk);
   const bf16_t* kb = kc + ((int64_t)b * H + h) * S * HD;
@@ -1092,7 +1092,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void x
   const int r = blockIdx.x - p.n_lin;
   const int row = r % rows, split = r / rows, ns = p.ns;
   const int h = row % p.H, b = row / p.H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
   const int k0 = split * p.chunk, k1 = min(p.S, k0 + p.chunk);
   const bf16_t* kb = p.kc + ((int64_t)b * p.H + h) * p.S * HD;
@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void c
   }
   const int row = blockIdx.x - (QG ? p.n_lin : 0);
   const int h = row % p.H, b = row / p.H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int sub = lane & 7, slot = wave * 8 + (lane >> 3);
   const bf16_t* kb = p.kc + ((int64_t)b * p.H + h) * p.S * HD;
   const bf16_t* vb = p.vc + ((int64_t)b * p.H + h) * p.S * HD;
@@ -1317,7 +1317,7 @@ __global__ __launch_bounds__(256) void cross_attn_multi_kernel(const T* __restri
   __shared__ float red[4][4][64];
   __shared__ float stat[4][8];
   __shared__ int last;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int ngrp = (q_len + QN - 1) / QN;
   const int h = blockIdx.x % H;
   const int bg = blockIdx.x / H;

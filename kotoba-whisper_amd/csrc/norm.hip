@@ -15,7 +15,7 @@ __global__ __launch_bounds__(256) void layernorm_kernel(float* __restrict__ x, i
                                                         const float* __restrict__ g, const float* __restrict__ bta,
                                                         float eps, TOut* __restrict__ y, const bf16_t* __restrict__ delta) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: one row per wave
   if (row >= rows) return;
   float4* xr = reinterpret_cast<float4*>(x + row * dim);
   const ushort4* dr = delta ? reinterpret_cast<const ushort4*>(delta + row * dim) : nullptr;
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void layernorm_bf16res_kernel(bf16_t* __restri
                                                                 const float* __restrict__ bta, float eps,
                                                                 TOut* __restrict__ y, const bf16_t* __restrict__ delta) {
   const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t row = (int64_t)blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // scalar: one row per wave
   if (row >= rows) return;
   uint4* xr = reinterpret_cast<uint4*>(x + row * dim);
   const uint4* dr = delta ? reinterpret_cast<const uint4*>(delta + row * dim) : nullptr;
