@@ -125,3 +125,6 @@ def test_integration_doc_names_only_declared_symbols():
         named |= {base + s for s in re.findall(r"`(_[a-z0-9_]+)`", rest)}
     missing = sorted(named - set(_declared()))
     assert named and not missing, missing
+    # and the other way round: every entry point the header declares is in the guide
+    undocumented = sorted(set(_declared()) - named)
+    assert not undocumented, undocumented
