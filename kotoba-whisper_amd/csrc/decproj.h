@@ -10,6 +10,11 @@
 #pragma once
 #include "kw_common.h"
 
+// development hook (tools/lab/qkv_stamps.hip defines it to record s_memrealtime per workgroup phase); no-op here
+#ifndef KW_PROJ_STAMP
+#define KW_PROJ_STAMP(slot)
+#endif
+
 namespace {
 
 constexpr int PROJ_KTM = 5;                      // k-tiles per virtual wave (dec_linear's choose() for K <= 1280)
@@ -47,6 +52,7 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int M = a.M, nkt = a.K >> 5;
   const int nv = (nkt + PROJ_KTM - 1) / PROJ_KTM;
+  KW_PROJ_STAMP(0);
   const bf16_t* x0 = a.x + (int64_t)min(lane & 15, M - 1) * a.ldx + (lane >> 4) * 8;
   const bf16_t* x1 = a.x + (int64_t)min(16 + (lane & 15), M - 1) * a.ldx + (lane >> 4) * 8;
   const int n_e = min(cg * 16 + (lane & 15), a.N - 1);
@@ -124,6 +130,7 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
     red[v][0][lane] = c0;
     red[v][1][lane] = c1;
   }
+  KW_PROJ_STAMP(1);
   __syncthreads();
   // r06: the two row halves' reduction, LayerNorm statistics and publish on waves 0 and 1 at once (each sums its half's
   // partial tiles in virtual-wave order and forms its rows' statistics itself: bitwise wave 0 alone doing both, as
@@ -163,6 +170,7 @@ __device__ __forceinline__ void proj_publish_granules(const ProjArgs& a, int cg,
       __hip_atomic_store(gran + (int64_t)m * (a.N / 2) + (n >> 1), (1ull << 32) | (mine | (other << 16)),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  KW_PROJ_STAMP(2);
 }
 
 }  // namespace

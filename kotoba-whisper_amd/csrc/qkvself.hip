@@ -23,6 +23,11 @@
 #include "attn_common.h"
 #include "decproj.h"
 
+// development hook (tools/lab/qkv_stamps.hip defines it to record s_memrealtime per workgroup phase); no-op here
+#ifndef KW_QS_STAMP
+#define KW_QS_STAMP(slot)
+#endif
+
 namespace {
 
 constexpr int QS_SPIN_LIMIT = 1 << 22;
@@ -58,6 +63,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void q
                           blockIdx.x, scratch, p.gran);
     return;
   }
+  KW_QS_STAMP(4);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // uniform (scalar branches)
   const int ps = wave >> 1, pw = wave & 1, ptid = tid & 127;  // pair slot (2 waves each), wave within it
   const int L = *p.cur_len;  // positions [0, L - 1) cached, L - 1 new
@@ -106,6 +112,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void q
     __hip_atomic_store(g, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm (single consumer)
   }
   __syncthreads();
+  KW_QS_STAMP(5);
   if (has_pair) {
     const uint32_t* st = stage[ps];
     const u32x4 qraw = {st[sub * 4], st[sub * 4 + 1], st[sub * 4 + 2], st[sub * 4 + 3]};
@@ -165,6 +172,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void q
       astat[ps][2 + pw] = lw;
     }
   }
+  KW_QS_STAMP(6);
   __syncthreads();
   if (has_pair && ptid < HD) {
     const float* st = astat[ps];
@@ -174,6 +182,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void q
     const float o = fmaf(ared[ps][0][ptid], f0, ared[ps][1][ptid] * f1);
     p.out[(int64_t)b * d + h * HD + ptid] = f2bf(o / l);
   }
+  KW_QS_STAMP(7);
 }
 
 size_t qs_gran_bytes(int64_t M, int64_t d) { return (size_t)M * (size_t)(3 * d / 2) * sizeof(unsigned long long); }
